@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark: all-pairs Needleman-Wunsch on MI355X, reference metric GCUPS.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload big13|c3|c4|c5]
+
+One "step" = the whole getMinimumPenalties job of the workload: every pair's
+fill + traceback + trim + SHA-512 on its rank's GPU/host, the ONE all-gather
+of result records across ranks (N>1, RCCL), and rank 0's hash chain.  Inputs
+(sequences) are resident in HBM before the timed region.  value = total DP
+cells of the job / max-over-ranks wall time per step (strong scaling: the
+workload is fixed, its pairs are LPT-sharded over N GPUs).
+
+Default workload = BASELINE.json configs[1]: mseq-big13-example.txt (k=13,
+78 pairs, 2.785e11 cells), the reference's own headline input; its answer
+hash is checked against the published one every run.
+
+Also reported (rank 0):
+  roofline      nw_fill (the dominant kernel): algorithmic bytes per launch
+                (4 B per DP cell, the reference's int32 matrix)
+                / the fill launch's duration from HIP events on the engine
+                stream; traffic = PMC-measured HBM bytes per launch when
+                profiles/<round>/pmc_summary.json exists (else null).
+  cpu_baseline  the reference's submitted MPI+OpenMP program (oracle/_ref/sub,
+                compiled from the reference sources) on a bounded sample of
+                the same workload, on this host's cores.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "multiple-sequence-alignment-openmp-openmpi_amd")
+ORACLE = os.path.join(REPO, "oracle")
+for p in (PKG, ORACLE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+
+METRIC = "DP cell-updates/s (GCUPS) on k-way SoP MSA; 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0
+BYTES_PER_CELL = 4.0
+
+
+def synth(k, L, seed=0):
+    """Seeded uniform ACGT (mt19937_64-style per-sequence seeds)."""
+    out = []
+    for s in range(k):
+        rng = np.random.Generator(np.random.MT19937(seed + s))
+        out.append(np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, L)].tobytes())
+    return out
+
+
+def load_workload(name):
+    import seqalign
+
+    if name == "big13":
+        text = open(os.path.join(REPO, "tests", "golden", "data", "mseq-big13-example.txt"), "rb").read()
+        pxy, pgap, genes = seqalign.parse_input(text)
+        gold = {c["name"]: c for c in json.load(open(os.path.join(REPO, "tests", "golden", "golden.json")))["cases"]}
+        return "mseq-big13-example.txt (k=13)", pxy, pgap, genes, gold["big13"]["hash"]
+    if name == "c3":
+        return "synthetic k=64 L=50000 ACGT", 3, 2, synth(64, 50000), None
+    if name == "c4":
+        return "synthetic k=256 L=8000 ACGT", 3, 2, synth(256, 8000), None
+    if name == "c5":
+        return "synthetic k=32 L=200000 ACGT", 3, 2, synth(32, 200000), None
+    raise SystemExit("unknown workload " + name)
+
+
+def cells_of(genes, ids):
+    import seqalign
+
+    L = [len(g) for g in genes]
+    tot = 0
+    for p in ids:
+        i, j = seqalign.pair_ij(int(p))
+        tot += L[i] * L[j]
+    return tot
+
+
+def cpu_baseline(genes, pxy, pgap, budget_s=30.0):
+    """Reference program (oracle/_ref/sub) on a bounded sample: the 5 shortest
+    sequences of the workload (their 10 pairs)."""
+    import oracle
+
+    order = sorted(range(len(genes)), key=lambda i: (len(genes[i]), i))[:5]
+    sample = [genes[i] for i in sorted(order)]
+    k = len(sample)
+    cells = sum(len(sample[i]) * len(sample[j]) for i in range(1, k) for j in range(i))
+    text = b"%d\n%d\n%d\n" % (pxy, pgap, k) + b"\n".join(sample) + b"\n"
+    desc = "%d shortest sequences (lengths %s), %d pairs, %.3g cells" % (
+        k, ",".join(str(len(s)) for s in sample), k * (k - 1) // 2, cells)
+    sub = os.path.join(oracle.REF_DIR, "sub")
+    if os.path.exists(sub):
+        try:
+            us, _, _ = oracle.run_cli(sub, text, timeout=600)
+            # sub forces 16 OpenMP threads per rank (sub:94,238,425): 15 compute + 1 master
+            return {"value": round(cells / us / 1e3, 4), "unit": "GCUPS", "cores": 16, "kind": "reference",
+                    "sample": "oracle/_ref/sub (submit/xuliny-seqalkway.cpp, singleton rank, 16 threads) on " + desc,
+                    "host_cpus": os.cpu_count()}
+        except Exception as e:  # fall through to the port
+            desc += " [reference binary failed: %s]" % str(e)[:120]
+    # port: the oracle CLI (single-thread restatement of skel) on the 3 shortest
+    sample = sample[:3]
+    k = len(sample)
+    cells = sum(len(sample[i]) * len(sample[j]) for i in range(1, k) for j in range(i))
+    text = b"%d\n%d\n%d\n" % (pxy, pgap, k) + b"\n".join(sample) + b"\n"
+    us, _, _ = oracle.run_cli(oracle.CLI, text, timeout=600)
+    return {"value": round(cells / us / 1e3, 4), "unit": "GCUPS", "cores": 1, "kind": "port",
+            "sample": "oracle/_build/nw_oracle (skel restatement, 1 thread) on %d sequences, %.3g cells" % (k, cells)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="big13")
+    ap.add_argument("--bits", type=int, default=0, help="force DP storage width (4/8/16/32)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import seqalign
+
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+
+        import dist as nwdist
+
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = tdist
+        device = torch.device("cuda", local)
+
+    name, pxy, pgap, genes, gold_hash = load_workload(args.workload)
+    k = len(genes)
+    P = k * (k - 1) // 2
+    lengths = [len(g) for g in genes]
+    total_cells = cells_of(genes, range(P))
+    eng = seqalign.Engine(device=local if world > 1 else 0, bits=args.bits, verbose=args.verbose)
+    eng.set_sequences(genes)  # sequences resident in HBM before timing
+    my_ids = seqalign.shard_pairs(lengths, rank, world) if world > 1 else np.arange(P, dtype=np.int64)
+
+    def step():
+        if world > 1:
+            pen, hs, _ = nwdist.align_sharded(eng.align_pairs, lengths, pxy, pgap, rank, world, device=device)
+        else:
+            pen, hs = eng.align_pairs(my_ids, pxy, pgap)
+        h = seqalign.chain_hash(hs) if rank == 0 else None
+        return pen, h
+
+    def sync():
+        if world > 1:
+            import torch
+
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    checked = None
+    for _ in range(args.warmup):
+        _, h = step()
+        if rank == 0 and gold_hash is not None:
+            checked = h == gold_hash
+    sync()
+    fills, traces = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        _, h = step()
+        st = eng.stats()
+        fills.append(st["fill_ms"])
+        traces.append(st["traceback_ms"])
+    sync()
+    dt = time.perf_counter() - t0
+    if rank == 0 and gold_hash is not None:
+        checked = (checked is not False) and h == gold_hash
+    if world > 1:
+        import torch
+
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    ms_step = dt / max(args.steps, 1) * 1e3
+    gcups = total_cells * args.steps / dt / 1e9
+    st = eng.stats()
+    my_cells = cells_of(genes, my_ids)
+    fill_ms = float(np.mean(fills)) if fills else float("nan")
+    launches = max(st["fill_launches"], 1)
+    per_launch_ms = fill_ms / launches
+    alg_bytes = my_cells * BYTES_PER_CELL / launches
+    achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_summary.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(args.workload, {}).get("hbm_bytes_per_fill_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": METRIC,
+        "value": round(gcups, 3),
+        "unit": "GCUPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "reference input file (mseq-big13-example.txt)" if args.workload == "big13" else "synthetic",
+        "config": {"workload": name, "pairs": P, "cells": total_cells, "pxy": pxy, "pgap": pgap,
+                   "storage_bits_per_cell": st["bits"], "mode": seqalign.MODES.get(st["mode"]),
+                   "parallelism": "pair-sharded dp%d (LPT), one RCCL all-gather" % world},
+        "answer_hash_ok": checked,
+        "kernel": {"fill_ms": round(fill_ms, 3), "traceback_ms": round(float(np.mean(traces)), 3),
+                   "fill_gcups": round(my_cells / (fill_ms * 1e-3) / 1e9, 2),
+                   "fill_launches_per_step": st["fill_launches"], "batches": st["batches"]},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "algorithmic_bytes_per_cell": BYTES_PER_CELL,
+                     "stored_bytes_per_cell": st["bits"] / 8.0},
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(genes, pxy, pgap)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,145 @@
+/*
+ * nwk.h -- C-ABI of the MI355X all-pairs Needleman-Wunsch engine.
+ *
+ * Drop-in boundary for the reference's hot path (paths relative to the
+ * reference repository yangxvlin/multiple-sequence-alignment-openMP-openMPI):
+ *
+ *   nwk_get_minimum_penalties  replaces  std::string getMinimumPenalties(
+ *        std::string *genes, int k, int pxy, int pgap, int *penalties)
+ *        seqalign-mpi-skeleton.cpp:13,117-175 / submit/xuliny-seqalkway.cpp:232-364
+ *   nwk_align_pairs            replaces  the per-rank worker loop
+ *        do_MPI_task(rank) + do_task(...)  submit/xuliny-seqalkway.cpp:369-417,183-227
+ *        (one call aligns a shard of canonical pair ids and returns the
+ *        per-pair result record {penalty, problemhash} of Packet, sub:126-130)
+ *   nwk_get_minimum_penalty    replaces  int getMinimumPenalty(std::string x,
+ *        std::string y, int pxy, int pgap, int *xans, int *yans)
+ *        seqalign-mpi-skeleton.cpp:14,186-280 (+ the trim at skel:135-154)
+ *   nwk_chain_hash             replaces  the hash chain at skel:159 / sub:334-337
+ *   nwk_sha512_hex             replaces  sw::sha512::calculate, sha512.hh:159-164
+ *
+ * Conventions: plain pointers and sizes, caller-owned buffers, no exceptions
+ * across the ABI.  Every function returns NWK_OK (0) or a negative NWK_E*
+ * code; nwk_last_error() gives a thread-local message.  A context owns one
+ * HIP device, its pooled HBM workspace and its streams; a context is not
+ * re-entrant (one host thread per context), separate contexts may run
+ * concurrently on different devices.
+ *
+ * Canonical pair order (skel:122-123): for i = 1..k-1, for j = 0..i-1, pair
+ * id p = i*(i-1)/2 + j; genes[i] gives the DP rows (x), genes[j] the columns
+ * (y).  There is no CPU fallback: every DP cell is computed by the HIP
+ * kernels; a call without a usable device fails with NWK_EDEVICE.
+ */
+#ifndef NWK_H
+#define NWK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NWK_OK 0
+#define NWK_EINVAL (-1)   /* bad argument */
+#define NWK_ENOMEM (-2)   /* host or device allocation failed */
+#define NWK_EDEVICE (-3)  /* no HIP device / HIP runtime error */
+#define NWK_EKERNEL (-4)  /* kernel reported a fault (hand-off timeout) */
+#define NWK_ECOMM (-5)    /* RCCL error */
+
+#define NWK_HASH_RAW 64   /* bytes of a raw SHA-512 digest */
+#define NWK_HASH_HEX 129  /* 128 lowercase hex chars + NUL */
+
+typedef struct nwk_ctx nwk_ctx;
+
+typedef struct nwk_opts {
+  int32_t device;            /* HIP device ordinal for nwk_ctx_create (default 0) */
+  int32_t ngpus;             /* nwk_get_minimum_penalties: devices to shard over (0 = 1) */
+  int32_t bits;              /* DP storage width 4/8/16/32; 0 = narrowest exact width */
+  int32_t host_threads;      /* SHA-512 / finalize threads; 0 = min(16, cores) */
+  int64_t workspace_bytes;   /* HBM budget per device; 0 = 92% of free memory */
+  int32_t verbose;           /* 1 = per-call statistics on stderr */
+  int32_t reserved[5];
+} nwk_opts;
+
+typedef struct nwk_stats {
+  double fill_ms;            /* device time of the fill kernels (HIP events) */
+  double traceback_ms;       /* device time of the traceback kernels */
+  double total_ms;           /* wall time of the call */
+  double cells;              /* sum of m*n over the pairs of the call */
+  int64_t matrix_bytes;      /* HBM bytes of the stored DP matrices */
+  int32_t batches;           /* workspace batches used */
+  int32_t bits;              /* storage width used */
+  int32_t mode;              /* 0 = profile, 1 = compare, 2 = literal */
+  int32_t fill_launches;     /* fill-kernel launches in the call */
+  int32_t reserved[4];
+} nwk_stats;
+
+/* Defaults for nwk_opts (device 0, auto everything). */
+void nwk_opts_default(nwk_opts *opts);
+
+/* Thread-local description of the last error. */
+const char *nwk_last_error(void);
+
+/* Number of visible HIP devices (0 when none). */
+int nwk_device_count(void);
+
+int nwk_ctx_create(const nwk_opts *opts, nwk_ctx **out);
+void nwk_ctx_destroy(nwk_ctx *ctx);
+
+/*
+ * Uploads the k sequences (concatenated in seqs, offsets[k+1]) to the
+ * context's device; replaces the previous set.  Bytes are compared as raw
+ * bytes (case-sensitive), exactly like std::string::operator[] in skel:215.
+ */
+int nwk_set_sequences(nwk_ctx *ctx, const uint8_t *seqs, const int64_t *offsets, int32_t k);
+
+/*
+ * The per-rank worker (sub:369-417): aligns pair_ids[0..npairs) of the
+ * current sequence set.  penalties[npairs] and problem_hash[npairs*64] (raw
+ * SHA-512 of sha512hex(align1) ++ sha512hex(align2), skel:155-157) are
+ * written in the order of pair_ids.
+ */
+int nwk_align_pairs(nwk_ctx *ctx, const int64_t *pair_ids, int64_t npairs, int32_t pxy,
+                    int32_t pgap, int32_t *penalties, uint8_t *problem_hash);
+
+/* Statistics of the context's last nwk_align_pairs call. */
+int nwk_last_stats(const nwk_ctx *ctx, nwk_stats *out);
+
+/*
+ * getMinimumPenalties (skel:117-175): aligns all k(k-1)/2 pairs, fills
+ * penalties[P] in canonical order and writes the chained answer hash into
+ * hash_hex[129] ("" when P == 0).  With opts->ngpus = G > 1 the pairs are
+ * cell-cost sharded over devices 0..G-1 (one host thread each) and the
+ * 72-byte result records are collected with one ncclAllGather over xGMI.
+ * opts may be NULL (defaults).
+ */
+int nwk_get_minimum_penalties(const uint8_t *seqs, const int64_t *offsets, int32_t k,
+                              int32_t pxy, int32_t pgap, int32_t *penalties, char *hash_hex,
+                              const nwk_opts *opts);
+
+/*
+ * getMinimumPenalty + trim (skel:186-280, 135-154) for one pair: a1/a2 get
+ * the trimmed alignment rows (capacity m+n bytes each, not NUL-terminated),
+ * *alen their length, *penalty = dp[m][n].
+ */
+int nwk_get_minimum_penalty(nwk_ctx *ctx, const uint8_t *x, int32_t m, const uint8_t *y,
+                            int32_t n, int32_t pxy, int32_t pgap, uint8_t *a1, uint8_t *a2,
+                            int32_t *alen, int32_t *penalty);
+
+/*
+ * Deterministic cell-cost shard of the P pairs of a sequence set over world
+ * ranks (LPT on m*n, ties by pair id).  Writes this rank's pair ids
+ * (ascending) to out_ids (capacity P) and their count to *out_n.
+ */
+int nwk_shard_pairs(const int64_t *offsets, int32_t k, int32_t rank, int32_t world,
+                    int64_t *out_ids, int64_t *out_n);
+
+/* Chain (skel:159): acc = sha512hex(acc ++ hex(problem_hash[p])), p = 0..P-1. */
+int nwk_chain_hash(const uint8_t *problem_hash, int64_t P, char *hash_hex);
+
+/* sw::sha512::calculate equivalent: lowercase hex digest of data[0..len). */
+void nwk_sha512_hex(const uint8_t *data, int64_t len, char *out_hex);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NWK_H */

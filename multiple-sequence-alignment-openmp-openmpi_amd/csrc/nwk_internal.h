@@ -1,0 +1,72 @@
+// nwk_internal.h -- shared between the HIP kernels and the host runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nwk {
+
+constexpr int kWave = 64;
+constexpr int kRows = 8;                  // DP rows per lane (R)
+constexpr int kBandRows = kWave * kRows;  // rows per band = one wave's task
+constexpr int kEPad = 64;                 // E entries before column 0
+
+// Recurrence variants (see DESIGN.md "Kernels").
+enum Mode : int {
+  kProfile = 0,  // |alphabet| <= 4, penalties >= 0: signed-byte substitution profile
+  kCompare = 1,  // any bytes, penalties >= 0: byte compare + select
+  kLiteral = 2,  // any penalties: skel:215-224 literally (match ? diag : min3)
+};
+
+// One pair of the batch.  All offsets are element offsets into the
+// batch-level arrays passed to the kernels.
+struct PairDesc {
+  int64_t x_off;    // codes of x (DP rows) in `codes`
+  int64_t y_off;    // codes of y (DP columns) in `codes`
+  int64_t e_off;    // E index of y's column-0 entry (E[e_off + a] packs y[a..a+3])
+  int64_t mat_off;  // first dword of this pair's stored matrix
+  int64_t bnd_off;  // first granule of this pair's band-boundary rows
+  int64_t ops_off;  // first byte of this pair's traceback op buffer (capacity m+n)
+  int32_t m, n;
+  int32_t nbands;   // ceil(m / kBandRows)
+  int32_t nchunks;  // ceil(n / 64): 64-column boundary chunks
+  int32_t sblocks;  // 64-step super-blocks per band = nchunks + 1
+  int32_t slot;     // index of this pair in the batch's result arrays
+};
+
+struct FillArgs {
+  const PairDesc* pairs;
+  const int2* tasks;       // {pair index, band}, dependency-ordered
+  int ntasks;
+  const uint8_t* codes;    // sequence codes (x rows)
+  const uint32_t* E;       // expanded column codes, 4 per dword
+  uint32_t* mat;           // packed G = H - (i+j)*pgap, W bits per cell
+  unsigned long long* bnd; // {epoch:32 | G:32} granules, one per boundary cell
+  unsigned* counter;       // task dequeue head
+  unsigned* err;           // nonzero = a hand-off timed out
+  unsigned epoch;
+  int K0, K1;              // diag increments in G-space: match, mismatch
+};
+
+struct TraceArgs {
+  const PairDesc* pairs;
+  int npairs;
+  const uint8_t* codes;
+  const uint32_t* mat;
+  uint8_t* ops;            // per pair, reversed: 'D','U','L'
+  int* oplen;              // per slot
+  int2* endij;             // per slot: (i, j) where the traced walk stopped
+  int K1;
+};
+
+// Launchers (nwk_kernels.hip).  bits in {4, 8, 16, 32}.
+hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStream_t s);
+hipError_t launch_traceback(int bits, const TraceArgs& a, hipStream_t s);
+int fill_blocks_per_cu(int mode, int bits);
+
+// Dwords of one band of the stored matrix.
+__host__ __device__ inline int64_t band_dwords(int bits, int sblocks) {
+  const int spd = 32 / bits;  // steps per dword
+  return (int64_t)sblocks * (64 / spd) * kRows * kWave;
+}
+
+}  // namespace nwk

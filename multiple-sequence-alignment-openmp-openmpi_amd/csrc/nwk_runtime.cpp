@@ -1,0 +1,798 @@
+// nwk_runtime.cpp -- host side of the C-ABI in include/nwk.h.
+//
+// Replaces, for the hot path of the reference (paths relative to the
+// reference repository):
+//   getMinimumPenalties / do_MPI_task / do_task   submit/xuliny-seqalkway.cpp:183-417
+//   trim + string build + hashes                  seqalign-mpi-skeleton.cpp:135-159
+// The MPI master/worker queue becomes: canonical pair ids -> HBM-budgeted
+// batches -> one persistent fill launch + one traceback launch per batch per
+// device -> host trim/SHA-512 on a thread pool -> (multi-GPU) one
+// ncclAllGather of 72-byte result records -> rank-0 hash chain.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/nwk.h"
+#include "nwk_internal.h"
+#include "sha512.h"
+
+using namespace nwk;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(e_ == hipErrorOutOfMemory ? NWK_ENOMEM : NWK_EDEVICE, "%s: %s (%s:%d)", \
+                  #expr, hipGetErrorString(e_), __FILE__, __LINE__);                       \
+  } while (0)
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
+
+// Canonical pair id -> (i, j), skel:122-123.
+inline void pair_ij(int64_t p, int* i, int* j) {
+  int64_t ii = (int64_t)((1.0 + std::sqrt(1.0 + 8.0 * (double)p)) / 2.0);
+  while (ii * (ii - 1) / 2 > p) --ii;
+  while ((ii + 1) * ii / 2 <= p) ++ii;
+  *i = (int)ii;
+  *j = (int)(p - ii * (ii - 1) / 2);
+}
+
+// Device buffer that only grows.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return NWK_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    HIP_TRY(hipMalloc(&p, bytes));
+    cap = bytes;
+    return NWK_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return NWK_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    HIP_TRY(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    cap = bytes;
+    return NWK_OK;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct PairWork {
+  int64_t id;       // canonical pair id
+  int64_t out;      // index in the caller's output arrays
+  int i, j;         // x = seq i (rows), y = seq j (columns)
+  int m, n;
+  int64_t mat_dw, bnd_gr, ops_b;  // footprint
+};
+
+}  // namespace
+
+struct nwk_ctx {
+  nwk_opts opts{};
+  int device = 0;
+  int cus = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {};
+  int64_t budget = 0;
+  unsigned epoch = 0;
+  int host_threads = 1;
+
+  // sequence set
+  int k = 0;
+  std::vector<int64_t> off;     // k+1
+  std::vector<uint8_t> seqs;    // raw bytes
+  int alpha = 0;                // distinct bytes
+  uint8_t code_of[256] = {};
+  std::vector<int64_t> c_off;   // code offset per sequence (8-aligned)
+  std::vector<int64_t> e_off;   // E index of column 0 per sequence
+  DevBuf d_codes[2];            // [0] profile codes, [1] raw bytes
+  DevBuf d_E[2];
+  bool built[2] = {false, false};
+
+  // batch buffers
+  DevBuf d_work;                // matrices | boundary granules | op strings
+  bool work_zeroed = false;
+  size_t work_zeroed_bytes = 0;
+  DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij;
+  HostBuf h_pairs, h_tasks, h_oplen, h_endij, h_ops;
+
+  nwk_stats stats{};
+};
+
+extern "C" {
+
+void nwk_opts_default(nwk_opts* o) {
+  memset(o, 0, sizeof *o);
+  o->device = 0;
+  o->ngpus = 1;
+}
+
+const char* nwk_last_error(void) { return g_err.c_str(); }
+
+int nwk_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+void nwk_ctx_destroy(nwk_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  for (auto& b : c->d_codes) b.release();
+  for (auto& b : c->d_E) b.release();
+  c->d_work.release();
+  c->d_pairs.release(); c->d_tasks.release(); c->d_ctl.release();
+  c->d_oplen.release(); c->d_endij.release();
+  c->h_pairs.release(); c->h_tasks.release(); c->h_oplen.release();
+  c->h_endij.release(); c->h_ops.release();
+  for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int nwk_ctx_create(const nwk_opts* opts, nwk_ctx** out) {
+  if (!out) return fail(NWK_EINVAL, "nwk_ctx_create: out is NULL");
+  *out = nullptr;
+  int ndev = nwk_device_count();
+  nwk_opts o;
+  nwk_opts_default(&o);
+  if (opts) o = *opts;
+  if (ndev <= 0) return fail(NWK_EDEVICE, "nwk_ctx_create: no HIP device visible");
+  if (o.device < 0 || o.device >= ndev) return fail(NWK_EINVAL, "nwk_ctx_create: device %d of %d", o.device, ndev);
+  if (o.bits != 0 && o.bits != 4 && o.bits != 8 && o.bits != 16 && o.bits != 32)
+    return fail(NWK_EINVAL, "nwk_ctx_create: bits must be 0/4/8/16/32");
+  std::unique_ptr<nwk_ctx> c(new nwk_ctx);
+  c->opts = o;
+  c->device = o.device;
+  HIP_TRY(hipSetDevice(c->device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, c->device));
+  c->cus = prop.multiProcessorCount;
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
+  size_t fr = 0, tot = 0;
+  HIP_TRY(hipMemGetInfo(&fr, &tot));
+  c->budget = o.workspace_bytes > 0 ? o.workspace_bytes : (int64_t)((double)fr * 0.92) - (512ll << 20);
+  if (c->budget < (64ll << 20)) c->budget = 64ll << 20;
+  unsigned hc = std::thread::hardware_concurrency();
+  c->host_threads = o.host_threads > 0 ? o.host_threads : (int)std::min(16u, hc ? hc : 1u);
+  HIP_TRY(c->d_ctl.ensure(256) == NWK_OK ? hipSuccess : hipErrorOutOfMemory);
+  *out = c.release();
+  return NWK_OK;
+}
+
+int nwk_set_sequences(nwk_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t k) {
+  if (!c || (k > 0 && (!seqs || !offsets)) || k < 0) return fail(NWK_EINVAL, "nwk_set_sequences: bad argument");
+  for (int s = 0; s < k; ++s)
+    if (offsets[s + 1] < offsets[s] || offsets[s + 1] - offsets[s] > (1 << 30))
+      return fail(NWK_EINVAL, "nwk_set_sequences: bad offsets at %d", s);
+  c->k = k;
+  const int64_t base = k ? offsets[0] : 0;
+  if (k) c->off.assign(offsets, offsets + k + 1);
+  else c->off.assign(1, 0);
+  const int64_t total = k ? offsets[k] - base : 0;
+  if (total) c->seqs.assign(seqs + base, seqs + base + total);
+  else c->seqs.clear();
+  for (auto& v : c->off) v -= base;
+  bool seen[256] = {};
+  for (uint8_t b : c->seqs) seen[b] = true;
+  c->alpha = 0;
+  for (int b = 0; b < 256; ++b)
+    if (seen[b]) c->code_of[b] = (uint8_t)c->alpha++;
+  c->built[0] = c->built[1] = false;
+  // layout: codes 8-aligned; E with kEPad entries before column 0 and 256 after the end
+  c->c_off.resize(k);
+  c->e_off.resize(k);
+  int64_t co = 0, eo = 0;
+  for (int s = 0; s < k; ++s) {
+    const int64_t L = c->off[s + 1] - c->off[s];
+    c->c_off[s] = co;
+    co += round_up(L + 8, 8);
+    c->e_off[s] = eo + kEPad;
+    eo += kEPad + L + 256;
+  }
+  return NWK_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Builds (once per sequence set and encoding) the device codes and the
+// expanded column array E: E[a] packs the encodings of y[a..a+3].
+// kind 0: profile codes (code*8 in E, code in codes); kind 1: raw bytes.
+int build_encoding(nwk_ctx* c, int kind) {
+  if (c->built[kind]) return NWK_OK;
+  const int k = c->k;
+  const int64_t ncodes = k ? c->c_off[k - 1] + round_up(c->off[k] - c->off[k - 1] + 8, 8) : 8;
+  const int64_t nE = k ? c->e_off[k - 1] - kEPad + kEPad + (c->off[k] - c->off[k - 1]) + 256 : 64;
+  std::vector<uint8_t> codes((size_t)ncodes, 0);
+  std::vector<uint32_t> E((size_t)nE, 0);
+  for (int s = 0; s < k; ++s) {
+    const uint8_t* y = c->seqs.data() + c->off[s];
+    const int64_t L = c->off[s + 1] - c->off[s];
+    uint8_t* cd = codes.data() + c->c_off[s];
+    for (int64_t a = 0; a < L; ++a) cd[a] = kind == 0 ? c->code_of[y[a]] : y[a];
+    uint32_t* e = E.data() + c->e_off[s];
+    for (int64_t a = -kEPad; a < L + 256 - kEPad; ++a) {
+      uint32_t v = 0;
+      for (int q = 0; q < 4; ++q) {
+        const int64_t t = a + q;
+        uint32_t b = 0;
+        if (t >= 0 && t < L) b = kind == 0 ? (uint32_t)c->code_of[y[t]] * 8u : y[t];
+        v |= b << (8 * q);
+      }
+      e[a] = v;
+    }
+  }
+  int rc;
+  if ((rc = c->d_codes[kind].ensure(codes.size())) != NWK_OK) return rc;
+  if ((rc = c->d_E[kind].ensure(E.size() * 4)) != NWK_OK) return rc;
+  HIP_TRY(hipMemcpy(c->d_codes[kind].p, codes.data(), codes.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->d_E[kind].p, E.data(), E.size() * 4, hipMemcpyHostToDevice));
+  c->built[kind] = true;
+  return NWK_OK;
+}
+
+struct Plan {
+  int mode, bits, kind;
+  int K0, K1;
+};
+
+int choose_plan(const nwk_ctx* c, int pxy, int pgap, Plan* pl) {
+  if (pxy < 0 || pgap < 0) {
+    pl->mode = kLiteral;
+    pl->bits = 32;
+  } else {
+    const int64_t span = 2 * (int64_t)pgap + pxy;  // max |difference| the traceback compares
+    int b = span < 16 ? 4 : span < 256 ? 8 : span < 65536 ? 16 : 32;
+    if (c->opts.bits > b) b = c->opts.bits;
+    pl->bits = b;
+    const int64_t k0 = -2 * (int64_t)pgap, k1 = (int64_t)pxy - 2 * (int64_t)pgap;
+    const bool bytes_ok = k0 >= -128 && k0 <= 127 && k1 >= -128 && k1 <= 127;
+    pl->mode = (c->alpha <= 4 && bytes_ok) ? kProfile : kCompare;
+  }
+  pl->kind = pl->mode == kProfile ? 0 : 1;
+  pl->K0 = (int)(-2 * (int64_t)pgap);
+  pl->K1 = (int)((int64_t)pxy - 2 * (int64_t)pgap);
+  return NWK_OK;
+}
+
+void footprint(PairWork* w, int bits) {
+  const int64_t nb = ceil_div(w->m, kBandRows);
+  const int64_t nch = ceil_div(w->n, 64);
+  w->mat_dw = nb * band_dwords(bits, (int)(nch + 1));
+  w->bnd_gr = (nb - 1) * nch * 64;
+  w->ops_b = round_up((int64_t)w->m + w->n, 16);
+}
+
+// Host finalize of one pair (skel:263-272 prefix, 135-157 trim/strings/hash;
+// the penalty is the cost of the traced path, which telescopes to dp[m][n]).
+struct Finalized {
+  int32_t penalty;
+  unsigned char hash[64];
+};
+
+void finalize_pair(const uint8_t* x, int m, const uint8_t* y, int n, int pxy, int pgap,
+                   const uint8_t* ops_rev, int nops, int ei, int ej, Finalized* out,
+                   std::vector<uint8_t>* a1o = nullptr, std::vector<uint8_t>* a2o = nullptr) {
+  const int64_t L0 = (int64_t)(ei > 0 ? ei : ej) + nops;
+  std::vector<uint8_t> a1((size_t)L0), a2((size_t)L0);
+  int64_t pen = 0;
+  int64_t q = 0;
+  if (ei > 0) {
+    for (int t = 0; t < ei; ++t, ++q) { a1[q] = x[t]; a2[q] = '_'; }
+    pen += (int64_t)ei * pgap;
+  } else if (ej > 0) {
+    for (int t = 0; t < ej; ++t, ++q) { a1[q] = '_'; a2[q] = y[t]; }
+    pen += (int64_t)ej * pgap;
+  }
+  int i = ei, j = ej;
+  for (int t = nops - 1; t >= 0; --t, ++q) {
+    const uint8_t op = ops_rev[t];
+    if (op == 'D') {
+      a1[q] = x[i]; a2[q] = y[j];
+      pen += x[i] == y[j] ? 0 : pxy;
+      ++i; ++j;
+    } else if (op == 'U') {
+      a1[q] = x[i]; a2[q] = '_';
+      pen += pgap;
+      ++i;
+    } else {
+      a1[q] = '_'; a2[q] = y[j];
+      pen += pgap;
+      ++j;
+    }
+  }
+  (void)m; (void)n;
+  // skel:137-144: keep what follows the last column that is '_' in both rows
+  int64_t start = 0;
+  for (int64_t t = L0 - 1; t >= 0; --t)
+    if (a1[t] == '_' && a2[t] == '_') { start = t + 1; break; }
+  const int64_t alen = L0 - start;
+  char hx[256];
+  sha512_hex(a1.data() + start, (size_t)alen, hx);
+  sha512_hex(a2.data() + start, (size_t)alen, hx + 128);
+  sha512_raw(hx, 256, out->hash);
+  out->penalty = (int32_t)pen;
+  if (a1o) a1o->assign(a1.begin() + start, a1.end());
+  if (a2o) a2o->assign(a2.begin() + start, a2.end());
+}
+
+template <class F>
+void parallel_for(int threads, int64_t n, F&& f) {
+  if (n <= 0) return;
+  if (threads <= 1 || n == 1) {
+    for (int64_t t = 0; t < n; ++t) f(t);
+    return;
+  }
+  std::atomic<int64_t> next{0};
+  std::vector<std::thread> th;
+  const int T = (int)std::min<int64_t>(threads, n);
+  for (int w = 0; w < T; ++w)
+    th.emplace_back([&]() {
+      for (;;) {
+        const int64_t t = next.fetch_add(1);
+        if (t >= n) break;
+        f(t);
+      }
+    });
+  for (auto& t : th) t.join();
+}
+
+// Core: aligns `work` (any order) and writes penalties/hashes at work[].out.
+// If strings != nullptr (single-pair API), also returns the alignment rows.
+int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32_t* penalties,
+               uint8_t* hashes, std::vector<uint8_t>* a1, std::vector<uint8_t>* a2) {
+  const double t_start = now_ms();
+  nwk_stats st{};
+  Plan pl;
+  choose_plan(c, pxy, pgap, &pl);
+  st.bits = pl.bits;
+  st.mode = pl.mode;
+  int rc;
+  HIP_TRY(hipSetDevice(c->device));
+
+  // Degenerate pairs (m == 0 or n == 0) have no DP cells: prefix only.
+  std::vector<PairWork> dp;
+  dp.reserve(work.size());
+  for (auto& w : work) {
+    st.cells += (double)w.m * (double)w.n;
+    if (w.m == 0 || w.n == 0) {
+      Finalized f;
+      const uint8_t* x = c->seqs.data() + c->off[w.i];
+      const uint8_t* y = c->seqs.data() + c->off[w.j];
+      finalize_pair(x, w.m, y, w.n, pxy, pgap, nullptr, 0, w.m, w.n, &f, a1, a2);
+      penalties[w.out] = f.penalty;
+      memcpy(hashes + 64 * w.out, f.hash, 64);
+    } else {
+      footprint(&w, pl.bits);
+      dp.push_back(w);
+    }
+  }
+  if (!dp.empty()) {
+    if ((rc = build_encoding(c, pl.kind)) != NWK_OK) return rc;
+  }
+  // Largest first (LPT inside the device; longest bands dequeued first).
+  std::sort(dp.begin(), dp.end(), [](const PairWork& a, const PairWork& b) {
+    const double ca = (double)a.m * a.n, cb = (double)b.m * b.n;
+    if (ca != cb) return ca > cb;
+    return a.id < b.id;
+  });
+  const int bpc = fill_blocks_per_cu(pl.mode, pl.bits);
+  const int grid = bpc * c->cus;
+  float ms = 0;
+
+  size_t pos = 0;
+  while (pos < dp.size()) {
+    // ---- form a batch that fits the HBM budget
+    size_t end = pos;
+    int64_t mat = 0, bnd = 0, ops = 0;
+    while (end < dp.size()) {
+      const PairWork& w = dp[end];
+      const int64_t need = (mat + w.mat_dw) * 4 + (bnd + w.bnd_gr) * 8 + ops + w.ops_b + 4096;
+      if (need > c->budget && end > pos) break;
+      if (need > c->budget)
+        return fail(NWK_ENOMEM, "pair %lld (%d x %d) needs %lld bytes > HBM budget %lld", (long long)w.id,
+                    w.m, w.n, (long long)need, (long long)c->budget);
+      mat += w.mat_dw; bnd += w.bnd_gr; ops += w.ops_b;
+      ++end;
+    }
+    const int np = (int)(end - pos);
+    const int64_t bnd_base_b = round_up(mat * 4, 256);
+    const int64_t ops_base_b = round_up(bnd_base_b + bnd * 8, 256);
+    const int64_t work_b = ops_base_b + ops + 256;
+    if ((rc = c->d_work.ensure((size_t)work_b)) != NWK_OK) return rc;
+    if (!c->work_zeroed || c->work_zeroed_bytes < c->d_work.cap) {
+      // granule tags must never hold a future epoch: zero once per allocation
+      HIP_TRY(hipMemsetAsync(c->d_work.p, 0, c->d_work.cap, c->stream));
+      c->work_zeroed = true;
+      c->work_zeroed_bytes = c->d_work.cap;
+    }
+    // ---- descriptors and dependency-ordered band tasks (band-major)
+    if ((rc = c->h_pairs.ensure(sizeof(PairDesc) * np)) != NWK_OK) return rc;
+    PairDesc* pd = c->h_pairs.as<PairDesc>();
+    int64_t mo = 0, bo = 0, oo = 0, ntasks = 0;
+    int maxb = 0;
+    for (int q = 0; q < np; ++q) {
+      const PairWork& w = dp[pos + q];
+      PairDesc& d = pd[q];
+      d.x_off = c->c_off[w.i];
+      d.y_off = c->c_off[w.j];
+      d.e_off = c->e_off[w.j];
+      d.mat_off = mo;
+      d.bnd_off = bnd_base_b / 8 + bo;
+      d.ops_off = ops_base_b + oo;
+      d.m = w.m;
+      d.n = w.n;
+      d.nbands = (int)ceil_div(w.m, kBandRows);
+      d.nchunks = (int)ceil_div(w.n, 64);
+      d.sblocks = d.nchunks + 1;
+      d.slot = q;
+      mo += w.mat_dw; bo += w.bnd_gr; oo += w.ops_b;
+      ntasks += d.nbands;
+      maxb = std::max(maxb, d.nbands);
+    }
+    if ((rc = c->h_tasks.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
+    int2* tk = c->h_tasks.as<int2>();
+    int64_t t = 0;
+    for (int b = 0; b < maxb; ++b)
+      for (int q = 0; q < np; ++q)
+        if (b < pd[q].nbands) tk[t++] = make_int2(q, b);
+    if ((rc = c->d_pairs.ensure(sizeof(PairDesc) * np)) != NWK_OK) return rc;
+    if ((rc = c->d_tasks.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
+    if ((rc = c->d_oplen.ensure(sizeof(int) * np)) != NWK_OK) return rc;
+    if ((rc = c->d_endij.ensure(sizeof(int2) * np)) != NWK_OK) return rc;
+    if ((rc = c->h_oplen.ensure(sizeof(int) * np)) != NWK_OK) return rc;
+    if ((rc = c->h_endij.ensure(sizeof(int2) * np)) != NWK_OK) return rc;
+    if ((rc = c->h_ops.ensure((size_t)ops)) != NWK_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(c->d_pairs.p, pd, sizeof(PairDesc) * np, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_tasks.p, tk, sizeof(int2) * ntasks, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_ctl.p, 0, 256, c->stream));
+
+    FillArgs fa;
+    fa.pairs = c->d_pairs.as<PairDesc>();
+    fa.tasks = c->d_tasks.as<int2>();
+    fa.ntasks = (int)ntasks;
+    fa.codes = c->d_codes[pl.kind].as<uint8_t>();
+    fa.E = c->d_E[pl.kind].as<uint32_t>();
+    fa.mat = c->d_work.as<uint32_t>();
+    fa.bnd = c->d_work.as<unsigned long long>();
+    fa.counter = c->d_ctl.as<unsigned>();
+    fa.err = c->d_ctl.as<unsigned>() + 16;
+    fa.epoch = ++c->epoch;
+    if (fa.epoch == 0) fa.epoch = ++c->epoch;
+    fa.K0 = pl.K0;
+    fa.K1 = pl.K1;
+    HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+    HIP_TRY(launch_fill(pl.mode, pl.bits, fa, std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    TraceArgs ta;
+    ta.pairs = fa.pairs;
+    ta.npairs = np;
+    ta.codes = fa.codes;
+    ta.mat = fa.mat;
+    ta.ops = c->d_work.as<uint8_t>();
+    ta.oplen = c->d_oplen.as<int>();
+    ta.endij = c->d_endij.as<int2>();
+    ta.K1 = pl.K1;
+    HIP_TRY(launch_traceback(pl.bits, ta, c->stream));
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    unsigned herr = 0;
+    HIP_TRY(hipMemcpyAsync(&herr, fa.err, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_oplen.p, ta.oplen, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_endij.p, ta.endij, sizeof(int2) * np, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_ops.p, c->d_work.as<uint8_t>() + ops_base_b, (size_t)ops, hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (herr) return fail(NWK_EKERNEL, "fill kernel: band hand-off timed out (err=%u)", herr);
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    st.fill_ms += ms;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
+    st.traceback_ms += ms;
+    st.matrix_bytes += mat * 4;
+    st.batches += 1;
+    st.fill_launches += 1;
+    // ---- host finalize
+    const int* ol = c->h_oplen.as<int>();
+    const int2* ej = c->h_endij.as<int2>();
+    const uint8_t* hops = c->h_ops.as<uint8_t>();
+    parallel_for(a1 ? 1 : c->host_threads, np, [&](int64_t q) {
+      const PairWork& w = dp[pos + q];
+      const PairDesc& d = pd[q];
+      Finalized f;
+      finalize_pair(c->seqs.data() + c->off[w.i], w.m, c->seqs.data() + c->off[w.j], w.n, pxy, pgap,
+                    hops + (d.ops_off - ops_base_b), ol[q], ej[q].x, ej[q].y, &f, a1, a2);
+      penalties[w.out] = f.penalty;
+      memcpy(hashes + 64 * w.out, f.hash, 64);
+    });
+    pos = end;
+  }
+  st.total_ms = now_ms() - t_start;
+  c->stats = st;
+  if (c->opts.verbose)
+    fprintf(stderr, "nwk: %zu pairs, %.3g cells, fill %.3f ms (%.1f GCUPS), traceback %.3f ms, total %.3f ms, bits %d mode %d, %d batch(es)\n",
+            work.size(), st.cells, st.fill_ms, st.fill_ms > 0 ? st.cells / st.fill_ms / 1e6 : 0.0,
+            st.traceback_ms, st.total_ms, st.bits, st.mode, st.batches);
+  return NWK_OK;
+}
+
+int make_work(const nwk_ctx* c, const int64_t* ids, int64_t n, std::vector<PairWork>* out) {
+  const int64_t P = (int64_t)c->k * (c->k - 1) / 2;
+  out->clear();
+  out->reserve((size_t)n);
+  for (int64_t q = 0; q < n; ++q) {
+    if (ids[q] < 0 || ids[q] >= P) return fail(NWK_EINVAL, "pair id %lld out of range [0,%lld)", (long long)ids[q], (long long)P);
+    PairWork w{};
+    w.id = ids[q];
+    w.out = q;
+    pair_ij(ids[q], &w.i, &w.j);
+    w.m = (int)(c->off[w.i + 1] - c->off[w.i]);
+    w.n = (int)(c->off[w.j + 1] - c->off[w.j]);
+    out->push_back(w);
+  }
+  return NWK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nwk_align_pairs(nwk_ctx* c, const int64_t* pair_ids, int64_t npairs, int32_t pxy, int32_t pgap,
+                    int32_t* penalties, uint8_t* problem_hash) {
+  if (!c || npairs < 0 || (npairs > 0 && (!pair_ids || !penalties || !problem_hash)))
+    return fail(NWK_EINVAL, "nwk_align_pairs: bad argument");
+  std::vector<PairWork> w;
+  int rc = make_work(c, pair_ids, npairs, &w);
+  if (rc != NWK_OK) return rc;
+  return align_work(c, w, pxy, pgap, penalties, problem_hash, nullptr, nullptr);
+}
+
+int nwk_last_stats(const nwk_ctx* c, nwk_stats* out) {
+  if (!c || !out) return fail(NWK_EINVAL, "nwk_last_stats: bad argument");
+  *out = c->stats;
+  return NWK_OK;
+}
+
+int nwk_get_minimum_penalty(nwk_ctx* c, const uint8_t* x, int32_t m, const uint8_t* y, int32_t n, int32_t pxy,
+                            int32_t pgap, uint8_t* a1, uint8_t* a2, int32_t* alen, int32_t* penalty) {
+  if (!c || m < 0 || n < 0 || (m && !x) || (n && !y) || !a1 || !a2 || !alen || !penalty)
+    return fail(NWK_EINVAL, "nwk_get_minimum_penalty: bad argument");
+  // set {y, x}: pair 0 = (i=1 -> rows x, j=0 -> columns y)
+  std::vector<uint8_t> s((size_t)m + n);
+  if (n) memcpy(s.data(), y, (size_t)n);
+  if (m) memcpy(s.data() + n, x, (size_t)m);
+  const int64_t off[3] = {0, n, (int64_t)n + m};
+  int rc = nwk_set_sequences(c, s.data(), off, 2);
+  if (rc != NWK_OK) return rc;
+  std::vector<PairWork> w;
+  const int64_t id = 0;
+  if ((rc = make_work(c, &id, 1, &w)) != NWK_OK) return rc;
+  std::vector<uint8_t> r1, r2;
+  unsigned char h[64];
+  if ((rc = align_work(c, w, pxy, pgap, penalty, h, &r1, &r2)) != NWK_OK) return rc;
+  memcpy(a1, r1.data(), r1.size());
+  memcpy(a2, r2.data(), r2.size());
+  *alen = (int32_t)r1.size();
+  return NWK_OK;
+}
+
+int nwk_shard_pairs(const int64_t* offsets, int32_t k, int32_t rank, int32_t world, int64_t* out_ids,
+                    int64_t* out_n) {
+  if (!offsets || k < 0 || world < 1 || rank < 0 || rank >= world || !out_n)
+    return fail(NWK_EINVAL, "nwk_shard_pairs: bad argument");
+  const int64_t P = (int64_t)k * (k - 1) / 2;
+  std::vector<std::pair<double, int64_t>> cost((size_t)P);
+  int64_t p = 0;
+  for (int i = 1; i < k; ++i)
+    for (int j = 0; j < i; ++j, ++p)
+      cost[p] = {(double)(offsets[i + 1] - offsets[i]) * (double)(offsets[j + 1] - offsets[j]) + 1.0, p};
+  std::sort(cost.begin(), cost.end(), [](const auto& a, const auto& b) {
+    return a.first != b.first ? a.first > b.first : a.second < b.second;
+  });
+  std::vector<double> load((size_t)world, 0.0);
+  int64_t cnt = 0;
+  for (const auto& cp : cost) {
+    int best = 0;
+    for (int r = 1; r < world; ++r)
+      if (load[r] < load[best]) best = r;
+    load[best] += cp.first;
+    if (best == rank) {
+      if (out_ids) out_ids[cnt] = cp.second;
+      ++cnt;
+    }
+  }
+  if (out_ids) std::sort(out_ids, out_ids + cnt);
+  *out_n = cnt;
+  return NWK_OK;
+}
+
+int nwk_chain_hash(const uint8_t* ph, int64_t P, char* hash_hex) {
+  if (!hash_hex || (P > 0 && !ph)) return fail(NWK_EINVAL, "nwk_chain_hash: bad argument");
+  char buf[256];
+  size_t la = 0;  // acc starts as "" (skel:121)
+  for (int64_t p = 0; p < P; ++p) {
+    to_hex(ph + 64 * p, buf + la);
+    char acc[128];
+    sha512_hex(buf, la + 128, acc);
+    memcpy(buf, acc, 128);
+    la = 128;
+  }
+  memcpy(hash_hex, buf, la);
+  hash_hex[la] = 0;
+  return NWK_OK;
+}
+
+void nwk_sha512_hex(const uint8_t* data, int64_t len, char* out_hex) {
+  sha512_hex(data, (size_t)len, out_hex);
+  out_hex[128] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// getMinimumPenalties: single device, or G devices + one ncclAllGather.
+// ---------------------------------------------------------------------------
+struct ResultRecord {
+  int32_t pair_id;
+  int32_t penalty;
+  uint8_t hash[64];
+};
+static_assert(sizeof(ResultRecord) == 72, "record layout");
+
+int nwk_get_minimum_penalties(const uint8_t* seqs, const int64_t* offsets, int32_t k, int32_t pxy, int32_t pgap,
+                              int32_t* penalties, char* hash_hex, const nwk_opts* opts) {
+  if (k < 0 || !hash_hex || (k > 0 && !offsets)) return fail(NWK_EINVAL, "nwk_get_minimum_penalties: bad argument");
+  nwk_opts o;
+  nwk_opts_default(&o);
+  if (opts) o = *opts;
+  const int64_t P = (int64_t)k * (k - 1) / 2;
+  if (P > 0 && !penalties) return fail(NWK_EINVAL, "nwk_get_minimum_penalties: penalties is NULL");
+  std::vector<uint8_t> ph((size_t)std::max<int64_t>(P, 1) * 64);
+  const int G = std::max(1, o.ngpus);
+  if (P == 0) {
+    hash_hex[0] = 0;
+    return NWK_OK;
+  }
+  if (G == 1) {
+    nwk_ctx* c = nullptr;
+    int rc = nwk_ctx_create(&o, &c);
+    if (rc != NWK_OK) return rc;
+    std::vector<int64_t> ids((size_t)P);
+    for (int64_t p = 0; p < P; ++p) ids[p] = p;
+    rc = nwk_set_sequences(c, seqs, offsets, k);
+    if (rc == NWK_OK) rc = nwk_align_pairs(c, ids.data(), P, pxy, pgap, penalties, ph.data());
+    nwk_ctx_destroy(c);
+    if (rc != NWK_OK) return rc;
+    return nwk_chain_hash(ph.data(), P, hash_hex);
+  }
+  if (G > nwk_device_count()) return fail(NWK_EINVAL, "ngpus=%d > visible devices %d", G, nwk_device_count());
+  // Shards: LPT on cell cost; every rank sends a padded block of `per` records.
+  std::vector<std::vector<int64_t>> shard((size_t)G);
+  int64_t per = 0;
+  for (int r = 0; r < G; ++r) {
+    int64_t n = 0;
+    shard[r].resize((size_t)P);
+    nwk_shard_pairs(offsets, k, r, G, shard[r].data(), &n);
+    shard[r].resize((size_t)n);
+    per = std::max(per, n);
+  }
+  std::vector<ncclComm_t> comms((size_t)G);
+  std::vector<int> devs((size_t)G);
+  for (int r = 0; r < G; ++r) devs[r] = r;
+  if (ncclCommInitAll(comms.data(), G, devs.data()) != ncclSuccess)
+    return fail(NWK_ECOMM, "ncclCommInitAll failed");
+  std::vector<ResultRecord> gathered((size_t)per * G);
+  std::vector<int> rcs((size_t)G, NWK_OK);
+  std::vector<std::string> errs((size_t)G);
+  std::vector<std::thread> th;
+  for (int r = 0; r < G; ++r) {
+    th.emplace_back([&, r]() {
+      nwk_opts ro = o;
+      ro.device = r;
+      nwk_ctx* c = nullptr;
+      int rc = nwk_ctx_create(&ro, &c);
+      const int64_t n = (int64_t)shard[r].size();
+      std::vector<ResultRecord> rec((size_t)per);
+      for (auto& x : rec) x.pair_id = -1;
+      if (rc == NWK_OK) rc = nwk_set_sequences(c, seqs, offsets, k);
+      std::vector<int32_t> pen((size_t)std::max<int64_t>(n, 1));
+      std::vector<uint8_t> hh((size_t)std::max<int64_t>(n, 1) * 64);
+      if (rc == NWK_OK && n > 0) rc = nwk_align_pairs(c, shard[r].data(), n, pxy, pgap, pen.data(), hh.data());
+      for (int64_t q = 0; rc == NWK_OK && q < n; ++q) {
+        rec[q].pair_id = (int32_t)shard[r][q];
+        rec[q].penalty = pen[q];
+        memcpy(rec[q].hash, hh.data() + 64 * q, 64);
+      }
+      // The collective runs even after a local failure (tagged records), so
+      // no rank is left waiting in ncclAllGather.
+      if (rc != NWK_OK) for (auto& x : rec) x.pair_id = -2;
+      (void)hipSetDevice(r);
+      void *dsend = nullptr, *drecv = nullptr;
+      hipStream_t s = nullptr;
+      int crc = NWK_OK;
+      if (hipMalloc(&dsend, sizeof(ResultRecord) * per) != hipSuccess ||
+          hipMalloc(&drecv, sizeof(ResultRecord) * per * G) != hipSuccess || hipStreamCreate(&s) != hipSuccess)
+        crc = NWK_ENOMEM;
+      if (crc == NWK_OK) {
+        if (hipMemcpy(dsend, rec.data(), sizeof(ResultRecord) * per, hipMemcpyHostToDevice) != hipSuccess) crc = NWK_EDEVICE;
+        if (ncclAllGather(dsend, drecv, sizeof(ResultRecord) * per, ncclUint8, comms[r], s) != ncclSuccess)
+          crc = NWK_ECOMM;
+        if (hipStreamSynchronize(s) != hipSuccess) crc = NWK_ECOMM;
+        if (r == 0 && crc == NWK_OK)
+          if (hipMemcpy(gathered.data(), drecv, sizeof(ResultRecord) * per * G, hipMemcpyDeviceToHost) != hipSuccess) crc = NWK_EDEVICE;
+      }
+      if (dsend) (void)hipFree(dsend);
+      if (drecv) (void)hipFree(drecv);
+      if (s) (void)hipStreamDestroy(s);
+      if (rc != NWK_OK) errs[r] = g_err;
+      rcs[r] = rc != NWK_OK ? rc : crc;
+      if (c) nwk_ctx_destroy(c);
+    });
+  }
+  for (auto& t : th) t.join();
+  for (auto& cm : comms) ncclCommDestroy(cm);
+  for (int r = 0; r < G; ++r)
+    if (rcs[r] != NWK_OK) return fail(rcs[r], "rank %d: %s", r, errs[r].empty() ? "collective failed" : errs[r].c_str());
+  std::vector<char> have((size_t)P, 0);
+  for (const auto& x : gathered) {
+    if (x.pair_id < 0) continue;
+    penalties[x.pair_id] = x.penalty;
+    memcpy(ph.data() + 64 * (int64_t)x.pair_id, x.hash, 64);
+    have[x.pair_id] = 1;
+  }
+  for (int64_t p = 0; p < P; ++p)
+    if (!have[p]) return fail(NWK_ECOMM, "pair %lld missing after all-gather", (long long)p);
+  return nwk_chain_hash(ph.data(), P, hash_hex);
+}
+
+}  // extern "C"

@@ -1,0 +1,257 @@
+"""Host-side mirror of the reference's hot-path interface over the C-ABI.
+
+The reference (yangxvlin/multiple-sequence-alignment-openMP-openMPI) exposes
+the path as three C++ functions; this module keeps their names, argument
+meaning and results, and runs every DP cell on the MI355X through
+``lib/libnwk.so`` (include/nwk.h).  There is no CPU fallback: without the
+built library or a HIP device the calls raise ``NwkError``.
+
+    getMinimumPenalties(genes, k, pxy, pgap, penalties) -> hash
+        seqalign-mpi-skeleton.cpp:117-175, submit/xuliny-seqalkway.cpp:232-364
+    getMinimumPenalty(x, y, pxy, pgap) -> (penalty, align1, align2)
+        seqalign-mpi-skeleton.cpp:186-280 + trim 135-154
+    do_MPI_task(...)  ->  Engine.align_pairs(pair_ids, ...)
+        submit/xuliny-seqalkway.cpp:369-417 (one rank's share of the pairs)
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libnwk.so")
+
+NWK_OK = 0
+ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "EKERNEL", -5: "ECOMM"}
+MODES = {0: "profile", 1: "compare", 2: "literal"}
+
+
+class NwkError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("nwk error %d (%s): %s" % (code, ERRORS.get(code, "?"), msg))
+        self.code = code
+
+
+class Opts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("ngpus", ctypes.c_int32), ("bits", ctypes.c_int32),
+                ("host_threads", ctypes.c_int32), ("workspace_bytes", ctypes.c_int64),
+                ("verbose", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("fill_ms", ctypes.c_double), ("traceback_ms", ctypes.c_double),
+                ("total_ms", ctypes.c_double), ("cells", ctypes.c_double),
+                ("matrix_bytes", ctypes.c_int64), ("batches", ctypes.c_int32),
+                ("bits", ctypes.c_int32), ("mode", ctypes.c_int32),
+                ("fill_launches", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
+
+
+# Every exported symbol of include/nwk.h with its ctypes signature.
+_P = ctypes.c_void_p
+_I32, _I64 = ctypes.c_int32, ctypes.c_int64
+SIGNATURES = {
+    "nwk_opts_default": (None, [_P]),
+    "nwk_last_error": (ctypes.c_char_p, []),
+    "nwk_device_count": (ctypes.c_int, []),
+    "nwk_ctx_create": (ctypes.c_int, [_P, _P]),
+    "nwk_ctx_destroy": (None, [_P]),
+    "nwk_set_sequences": (ctypes.c_int, [_P, _P, _P, _I32]),
+    "nwk_align_pairs": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P]),
+    "nwk_last_stats": (ctypes.c_int, [_P, _P]),
+    "nwk_get_minimum_penalties": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P]),
+    "nwk_get_minimum_penalty": (ctypes.c_int, [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
+    "nwk_shard_pairs": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
+    "nwk_chain_hash": (ctypes.c_int, [_P, _I64, _P]),
+    "nwk_sha512_hex": (None, [_P, _I64, _P]),
+}
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Loads lib/libnwk.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise NwkError(-3, "HIP extension not built: %s (run __graft_entry__.build())" % path)
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc):
+    if rc != NWK_OK:
+        raise NwkError(rc, _lib.nwk_last_error().decode("utf-8", "replace"))
+
+
+def _as_bytes(s):
+    if isinstance(s, bytes):
+        return s
+    if isinstance(s, str):
+        return s.encode("latin-1")
+    return bytes(s)
+
+
+def pack_genes(genes):
+    """Concatenated bytes + int64 offsets[k+1] (the C-ABI's sequence set)."""
+    bs = [_as_bytes(g) for g in genes]
+    offs = np.zeros(len(bs) + 1, dtype=np.int64)
+    if bs:
+        offs[1:] = np.cumsum([len(b) for b in bs])
+    data = np.frombuffer(b"".join(bs) or b"\0", dtype=np.uint8).copy()
+    return data, offs
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def device_count():
+    return load_library().nwk_device_count()
+
+
+def pair_index(i, j):
+    """Canonical pair id of (i, j), i > j (skel:122-123)."""
+    return i * (i - 1) // 2 + j
+
+
+def pair_ij(p):
+    i = int((1 + (1 + 8 * p) ** 0.5) // 2)
+    while i * (i - 1) // 2 > p:
+        i -= 1
+    while (i + 1) * i // 2 <= p:
+        i += 1
+    return i, p - i * (i - 1) // 2
+
+
+class Engine:
+    """One device context: pooled HBM workspace + streams (nwk_ctx)."""
+
+    def __init__(self, device=0, bits=0, workspace_bytes=0, host_threads=0, verbose=False):
+        self.lib = load_library()
+        o = Opts()
+        self.lib.nwk_opts_default(ctypes.byref(o))
+        o.device, o.bits, o.workspace_bytes = device, bits, workspace_bytes
+        o.host_threads, o.verbose = host_threads, int(verbose)
+        self._ctx = ctypes.c_void_p()
+        _check(self.lib.nwk_ctx_create(ctypes.byref(o), ctypes.byref(self._ctx)))
+        self.k = 0
+        self._offs = None
+
+    def close(self):
+        if self._ctx:
+            self.lib.nwk_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_sequences(self, genes):
+        data, offs = pack_genes(genes)
+        _check(self.lib.nwk_set_sequences(self._ctx, _ptr(data), _ptr(offs), len(genes)))
+        self.k = len(genes)
+        self._offs = offs
+
+    def align_pairs(self, pair_ids, pxy, pgap):
+        """The worker loop of one rank: returns (penalties int32[n], raw hashes uint8[n,64])."""
+        ids = np.ascontiguousarray(pair_ids, dtype=np.int64)
+        n = ids.size
+        pen = np.zeros(max(n, 1), dtype=np.int32)
+        hs = np.zeros((max(n, 1), 64), dtype=np.uint8)
+        _check(self.lib.nwk_align_pairs(self._ctx, _ptr(ids), n, pxy, pgap, _ptr(pen), _ptr(hs)))
+        return pen[:n], hs[:n]
+
+    def stats(self):
+        s = Stats()
+        _check(self.lib.nwk_last_stats(self._ctx, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in Stats._fields_ if f != "reserved"}
+
+    def get_minimum_penalty(self, x, y, pxy, pgap):
+        xb, yb = _as_bytes(x), _as_bytes(y)
+        m, n = len(xb), len(yb)
+        a1 = ctypes.create_string_buffer(max(m + n, 1))
+        a2 = ctypes.create_string_buffer(max(m + n, 1))
+        alen, pen = ctypes.c_int32(), ctypes.c_int32()
+        _check(self.lib.nwk_get_minimum_penalty(self._ctx, xb, m, yb, n, pxy, pgap, a1, a2,
+                                                ctypes.byref(alen), ctypes.byref(pen)))
+        self.k = 2
+        return pen.value, a1.raw[:alen.value], a2.raw[:alen.value]
+
+
+def chain_hash(problem_hashes):
+    """skel:159 chain over raw 64-byte problem hashes in canonical order."""
+    lib = load_library()
+    h = np.ascontiguousarray(problem_hashes, dtype=np.uint8).reshape(-1, 64)
+    out = ctypes.create_string_buffer(129)
+    _check(lib.nwk_chain_hash(_ptr(h), h.shape[0], out))
+    return out.value.decode()
+
+
+def sha512_hex(data):
+    lib = load_library()
+    b = _as_bytes(data)
+    out = ctypes.create_string_buffer(129)
+    lib.nwk_sha512_hex(b, len(b), out)
+    return out.value.decode()
+
+
+def shard_pairs(lengths, rank, world):
+    """This rank's canonical pair ids under the engine's LPT cell-cost shard."""
+    lib = load_library()
+    offs = np.zeros(len(lengths) + 1, dtype=np.int64)
+    if len(lengths):
+        offs[1:] = np.cumsum(lengths)
+    k = len(lengths)
+    P = k * (k - 1) // 2
+    out = np.zeros(max(P, 1), dtype=np.int64)
+    n = ctypes.c_int64()
+    _check(lib.nwk_shard_pairs(_ptr(offs), k, rank, world, _ptr(out), ctypes.byref(n)))
+    return out[:n.value].copy()
+
+
+def getMinimumPenalties(genes, k, pxy, pgap, penalties, ngpus=1, bits=0, verbose=False):
+    """skel:117-175: fills penalties[0..P) in canonical order, returns the hash."""
+    lib = load_library()
+    genes = list(genes)[:k]
+    data, offs = pack_genes(genes)
+    P = k * (k - 1) // 2
+    pen = np.zeros(max(P, 1), dtype=np.int32)
+    out = ctypes.create_string_buffer(129)
+    o = Opts()
+    lib.nwk_opts_default(ctypes.byref(o))
+    o.ngpus, o.bits, o.verbose = ngpus, bits, int(verbose)
+    _check(lib.nwk_get_minimum_penalties(_ptr(data), _ptr(offs), k, pxy, pgap, _ptr(pen), out,
+                                         ctypes.byref(o)))
+    for p in range(P):
+        penalties[p] = int(pen[p])
+    return out.value.decode()
+
+
+def getMinimumPenalty(x, y, pxy, pgap, device=0):
+    """skel:186-280 + trim: (penalty, align1, align2) for one pair."""
+    with Engine(device=device) as e:
+        return e.get_minimum_penalty(x, y, pxy, pgap)
+
+
+def parse_input(text):
+    """Rank-0 stdin parse of skel:40-47 (cin >> tokens): (pxy, pgap, genes)."""
+    if isinstance(text, str):
+        text = text.encode("latin-1")
+    tok = text.split()
+    pxy, pgap, k = int(tok[0]), int(tok[1]), int(tok[2])
+    genes = [tok[3 + i] if 3 + i < len(tok) else b"" for i in range(max(k, 0))]
+    return pxy, pgap, genes

@@ -1,0 +1,302 @@
+/*
+ * oracle/nw_oracle.c -- CPU restatement of the reference's all-pairs
+ * Needleman-Wunsch path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load or run anything built from this file, and only as the checker.  The
+ * product (multiple-sequence-alignment-openmp-openmpi_amd/) never links it.
+ *
+ * What it restates (paths relative to the reference repository):
+ *   nwo_pair()        seqalign-mpi-skeleton.cpp:186-280  getMinimumPenalty
+ *                       fill 211-226, traceback 236-262, prefix 263-272
+ *                     + seqalign-mpi-skeleton.cpp:135-154 trim / build strings
+ *   nwo_problem_hash  seqalign-mpi-skeleton.cpp:155-157 (sha512 of the two
+ *                     hex digests, concatenated)
+ *   nwo_all()         seqalign-mpi-skeleton.cpp:117-175  getMinimumPenalties
+ *                     (canonical i=1..k-1, j=0..i-1 order, hash chain at 159)
+ *   main()            seqalign-mpi-skeleton.cpp:35-76 stdin/stdout contract
+ *   nwo_sha512_hex    sha512.hh:59-296 (a fresh FIPS 180-4 SHA-512; the
+ *                     reference encodes only the low 32 bits of the bit
+ *                     length, sha512.hh:131/141, which is the standard value
+ *                     for every message shorter than 2^29 bytes)
+ *
+ * Pinning: tests/test_oracle.py checks this file against the golden vectors
+ * in tests/golden/ (Project2B.pdf p.7, testing3/sequential.txt:2-3,
+ * the testing15 .out files, and outputs of the reference skeleton compiled here by
+ * oracle/build_ref.sh).
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/time.h>
+
+/* ------------------------------------------------------------------------ */
+/* SHA-512 (FIPS 180-4)                                                      */
+/* ------------------------------------------------------------------------ */
+static const uint64_t K512[80] = {
+    0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+    0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+    0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+    0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+    0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+    0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+    0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+    0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+    0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+    0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+    0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+    0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+    0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+    0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+    0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+    0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+    0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+    0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+    0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+    0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+#define ROR64(x, n) (((x) >> (n)) | ((x) << (64 - (n))))
+
+static void sha512_block(uint64_t st[8], const unsigned char *p) {
+  uint64_t w[80];
+  for (int t = 0; t < 16; ++t) {
+    uint64_t v = 0;
+    for (int b = 0; b < 8; ++b) v = (v << 8) | p[8 * t + b];
+    w[t] = v;
+  }
+  for (int t = 16; t < 80; ++t) {
+    uint64_t s0 = ROR64(w[t - 15], 1) ^ ROR64(w[t - 15], 8) ^ (w[t - 15] >> 7);
+    uint64_t s1 = ROR64(w[t - 2], 19) ^ ROR64(w[t - 2], 61) ^ (w[t - 2] >> 6);
+    w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+  }
+  uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+  for (int t = 0; t < 80; ++t) {
+    uint64_t S1 = ROR64(e, 14) ^ ROR64(e, 18) ^ ROR64(e, 41);
+    uint64_t ch = (e & f) ^ (~e & g);
+    uint64_t t1 = h + S1 + ch + K512[t] + w[t];
+    uint64_t S0 = ROR64(a, 28) ^ ROR64(a, 34) ^ ROR64(a, 39);
+    uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint64_t t2 = S0 + mj;
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+  st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+/* Lowercase 128-hex digest of data[0..len) into out[0..128] (NUL-terminated). */
+void nwo_sha512_hex(const unsigned char *data, size_t len, char out[129]) {
+  uint64_t st[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                    0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                    0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  size_t full = len / 128;
+  for (size_t i = 0; i < full; ++i) sha512_block(st, data + 128 * i);
+  unsigned char tail[256];
+  size_t rem = len - full * 128;
+  memset(tail, 0, sizeof tail);
+  if (rem) memcpy(tail, data + full * 128, rem);
+  tail[rem] = 0x80;
+  size_t tl = (rem + 1 + 16 <= 128) ? 128 : 256;
+  uint64_t bits = (uint64_t)len * 8u;
+  for (int b = 0; b < 8; ++b) tail[tl - 1 - b] = (unsigned char)(bits >> (8 * b));
+  sha512_block(st, tail);
+  if (tl == 256) sha512_block(st, tail + 128);
+  static const char hx[] = "0123456789abcdef";
+  for (int i = 0; i < 8; ++i)
+    for (int b = 0; b < 8; ++b) {
+      unsigned v = (unsigned)(st[i] >> (56 - 8 * b)) & 0xffu;
+      out[16 * i + 2 * b] = hx[v >> 4];
+      out[16 * i + 2 * b + 1] = hx[v & 15];
+    }
+  out[128] = 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Pairwise NW: seqalign-mpi-skeleton.cpp:186-280 plus trim 135-154          */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * Aligns x (rows, length m) against y (columns, length n).  a1/a2 must hold
+ * m+n bytes each.  On return *alen is the trimmed alignment length and the
+ * function returns dp[m][n].  Returns INT32_MIN if the DP matrix could not be
+ * allocated (the reference exits at skel:102-106).
+ */
+int nwo_pair(const unsigned char *x, int m, const unsigned char *y, int n, int pxy, int pgap,
+             unsigned char *a1, unsigned char *a2, int *alen) {
+  size_t W = (size_t)n + 1;
+  int *dp = (int *)malloc(sizeof(int) * (size_t)(m + 1) * W);
+  if (!dp) return INT32_MIN;
+#define DP(i, j) dp[(size_t)(i) * W + (size_t)(j)]
+  /* skel:201-208 */
+  for (int i = 0; i <= m; ++i) DP(i, 0) = i * pgap;
+  for (int j = 0; j <= n; ++j) DP(0, j) = j * pgap;
+  /* skel:211-226 (min3 at skel:83-91 returns the first minimum; for ints
+     the value is what matters) */
+  for (int i = 1; i <= m; ++i) {
+    const unsigned char xi = x[i - 1];
+    for (int j = 1; j <= n; ++j) {
+      if (xi == y[j - 1]) {
+        DP(i, j) = DP(i - 1, j - 1);
+      } else {
+        int a = DP(i - 1, j - 1) + pxy, b = DP(i - 1, j) + pgap, c = DP(i, j - 1) + pgap;
+        int mn = a;
+        if (b < mn) mn = b;
+        if (c < mn) mn = c;
+        DP(i, j) = mn;
+      }
+    }
+  }
+  /* skel:229-272: traceback into 1-indexed xans/yans of length l = m+n,
+     filled from position l downwards. */
+  int l = m + n;
+  int *xans = (int *)malloc(sizeof(int) * (size_t)(l + 1));
+  int *yans = (int *)malloc(sizeof(int) * (size_t)(l + 1));
+  if (!xans || !yans) { free(dp); free(xans); free(yans); return INT32_MIN; }
+  int i = m, j = n, xpos = l, ypos = l;
+  while (!(i == 0 || j == 0)) {
+    if (x[i - 1] == y[j - 1]) {
+      xans[xpos--] = x[i - 1]; yans[ypos--] = y[j - 1]; i--; j--;
+    } else if (DP(i - 1, j - 1) + pxy == DP(i, j)) {
+      xans[xpos--] = x[i - 1]; yans[ypos--] = y[j - 1]; i--; j--;
+    } else if (DP(i - 1, j) + pgap == DP(i, j)) {
+      xans[xpos--] = x[i - 1]; yans[ypos--] = '_'; i--;
+    } else if (DP(i, j - 1) + pgap == DP(i, j)) {
+      xans[xpos--] = '_'; yans[ypos--] = y[j - 1]; j--;
+    } else {
+      /* unreachable for a consistent DP (the reference would spin here) */
+      free(dp); free(xans); free(yans); return INT32_MIN;
+    }
+  }
+  while (xpos > 0) { if (i > 0) xans[xpos--] = x[--i]; else xans[xpos--] = '_'; }
+  while (ypos > 0) { if (j > 0) yans[ypos--] = y[--j]; else yans[ypos--] = '_'; }
+  int ret = DP(m, n);
+#undef DP
+  free(dp);
+  /* skel:135-144: id = one past the highest position holding '_' in both */
+  int id = 1;
+  for (int a = l; a >= 1; a--) {
+    if ((char)yans[a] == '_' && (char)xans[a] == '_') { id = a + 1; break; }
+  }
+  /* skel:145-154 */
+  int L = 0;
+  for (int a = id; a <= l; a++, L++) {
+    a1[L] = (unsigned char)xans[a];
+    a2[L] = (unsigned char)yans[a];
+  }
+  *alen = L;
+  free(xans); free(yans);
+  return ret;
+}
+
+/* skel:155-157: problemhash = sha512(sha512(a1) ++ sha512(a2)), hex. */
+void nwo_problem_hash(const unsigned char *a1, const unsigned char *a2, int alen, char out[129]) {
+  char buf[257];
+  nwo_sha512_hex(a1, (size_t)alen, buf);
+  nwo_sha512_hex(a2, (size_t)alen, buf + 128);
+  nwo_sha512_hex((const unsigned char *)buf, 256, out);
+}
+
+/* skel:159 over canonical order: acc = sha512(acc ++ problemhash[p]).
+   hashes is P*128 hex chars.  out is "" (out[0]==0) for P == 0. */
+void nwo_chain(const char *hashes, long P, char out[129]) {
+  char buf[257];
+  out[0] = 0;
+  for (long p = 0; p < P; ++p) {
+    size_t la = strlen(out);
+    memcpy(buf, out, la);
+    memcpy(buf + la, hashes + 128 * p, 128);
+    nwo_sha512_hex((const unsigned char *)buf, la + 128, out);
+  }
+}
+
+/*
+ * skel:117-175 getMinimumPenalties.  seqs is the concatenation of the k
+ * sequences, offsets has k+1 entries.  penalties[P], pair_hashes[P*128]
+ * (may be NULL) and out_hash[129] are caller-owned.  Returns 0 or -1 (OOM).
+ */
+int nwo_all(const unsigned char *seqs, const int64_t *offsets, int k, int pxy, int pgap,
+            int *penalties, char *pair_hashes, char out_hash[129]) {
+  long P = (long)k * (k - 1) / 2;
+  char *hs = pair_hashes ? pair_hashes : (char *)calloc((size_t)(P > 0 ? P : 1), 128);
+  if (!hs) return -1;
+  long p = 0;
+  for (int i = 1; i < k; ++i)
+    for (int j = 0; j < i; ++j, ++p) {
+      const unsigned char *x = seqs + offsets[i];
+      const unsigned char *y = seqs + offsets[j];
+      int m = (int)(offsets[i + 1] - offsets[i]);
+      int n = (int)(offsets[j + 1] - offsets[j]);
+      unsigned char *a1 = (unsigned char *)malloc((size_t)(m + n) + 1);
+      unsigned char *a2 = (unsigned char *)malloc((size_t)(m + n) + 1);
+      int alen = 0;
+      int pen = a1 && a2 ? nwo_pair(x, m, y, n, pxy, pgap, a1, a2, &alen) : INT32_MIN;
+      if (pen == INT32_MIN) { free(a1); free(a2); if (!pair_hashes) free(hs); return -1; }
+      penalties[p] = pen;
+      char ph[129];
+      nwo_problem_hash(a1, a2, alen, ph);
+      memcpy(hs + 128 * p, ph, 128);
+      free(a1); free(a2);
+    }
+  nwo_chain(hs, P, out_hash);
+  if (!pair_hashes) free(hs);
+  return 0;
+}
+
+#ifdef NWO_MAIN
+/* skel:35-76: rank-0 stdin parse (cin >> tokens), timer, output format. */
+static char *read_token(FILE *f, size_t *len) {
+  int c;
+  do { c = fgetc(f); } while (c == ' ' || c == '\n' || c == '\t' || c == '\r' || c == '\v' || c == '\f');
+  if (c == EOF) return NULL;
+  size_t cap = 64, n = 0;
+  char *s = (char *)malloc(cap);
+  while (c != EOF && !(c == ' ' || c == '\n' || c == '\t' || c == '\r' || c == '\v' || c == '\f')) {
+    if (n + 1 >= cap) { cap *= 2; s = (char *)realloc(s, cap); }
+    s[n++] = (char)c;
+    c = fgetc(f);
+  }
+  s[n] = 0;
+  *len = n;
+  return s;
+}
+
+int main(void) {
+  size_t tl;
+  char *t;
+  int pxy, pgap, k;
+  t = read_token(stdin, &tl); if (!t) return 1; pxy = atoi(t); free(t);
+  t = read_token(stdin, &tl); if (!t) return 1; pgap = atoi(t); free(t);
+  t = read_token(stdin, &tl); if (!t) return 1; k = atoi(t); free(t);
+  if (k < 0) k = 0;
+  int64_t *off = (int64_t *)malloc(sizeof(int64_t) * (size_t)(k + 1));
+  size_t cap = 1 << 16, used = 0;
+  unsigned char *seqs = (unsigned char *)malloc(cap);
+  off[0] = 0;
+  for (int i = 0; i < k; ++i) {
+    t = read_token(stdin, &tl);
+    if (!t) { tl = 0; t = (char *)calloc(1, 1); }
+    while (used + tl + 1 > cap) { cap *= 2; seqs = (unsigned char *)realloc(seqs, cap); }
+    memcpy(seqs + used, t, tl);
+    used += tl;
+    off[i + 1] = (int64_t)used;
+    free(t);
+  }
+  long P = (long)k * (k - 1) / 2;
+  int *pen = (int *)malloc(sizeof(int) * (size_t)(P > 0 ? P : 1));
+  char hash[129];
+  struct timeval tv0, tv1;
+  gettimeofday(&tv0, NULL);
+  if (nwo_all(seqs, off, k, pxy, pgap, pen, NULL, hash) != 0) {
+    fprintf(stderr, "getMinimumPenalty: new failed\n");
+    return 1;
+  }
+  gettimeofday(&tv1, NULL);
+  long us = (long)((tv1.tv_sec - tv0.tv_sec) * 1000000L + (tv1.tv_usec - tv0.tv_usec));
+  printf("Time: %ld us\n", us);
+  printf("%s\n", hash);
+  for (long p = 0; p < P; ++p) printf("%d ", pen[p]);
+  printf("\n");
+  free(pen); free(seqs); free(off);
+  return 0;
+}
+#endif

@@ -1,0 +1,182 @@
+"""GPU parity: the HIP path through the C-ABI against golden vectors and the oracle.
+
+Bar: bit-exact (penalties, per-pair problemhash, alignment strings, answer
+hash) -- this is integer/byte work.  Full-size inputs (big13 and its
+permutation, 2.785e11 cells each) are checked against the reference's
+published answers.
+"""
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+import seqalign
+from conftest import GOLDEN_DIR, PKG, case_input, load_golden
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = load_golden()
+
+
+@pytest.fixture(scope="module")
+def engine():
+    if seqalign.device_count() < 1:
+        pytest.fail("no HIP device visible for a -m gpu run")
+    e = seqalign.Engine(device=0)
+    yield e
+    e.close()
+
+
+def _all_ids(k):
+    return np.arange(k * (k - 1) // 2, dtype=np.int64)
+
+
+@pytest.mark.parametrize("case", GOLDEN, ids=[c["name"] for c in GOLDEN])
+def test_golden_cases(engine, case):
+    pxy, pgap, genes = case_input(case)
+    engine.set_sequences(genes)
+    k = len(genes)
+    pen, hs = engine.align_pairs(_all_ids(k), pxy, pgap)
+    assert [int(v) for v in pen] == case["penalties"]
+    if "pairs" in case:
+        assert [h.tobytes().hex() for h in hs] == [p["problemhash"] for p in case["pairs"]]
+    assert seqalign.chain_hash(hs) == case["hash"]
+
+
+def _rand_genes(r, k, lo, hi, alpha):
+    return [bytes(r.choice(alpha) for _ in range(r.randint(lo, hi))) for _ in range(k)]
+
+
+def _mutants(r, base, k, alpha):
+    out = []
+    for _ in range(k):
+        s = bytearray()
+        for c in base:
+            u = r.random()
+            if u < 0.02:
+                continue
+            if u < 0.04:
+                s.append(r.choice(alpha))
+            s.append(r.choice(alpha) if r.random() < 0.1 else c)
+        out.append(bytes(s))
+    return out
+
+
+PENALTIES = [(3, 2), (5, 1), (0, 0), (1, 0), (0, 1), (2, 7), (11, 2), (100, 70), (-1, 2), (3, -1), (-2, -3),
+             (40000, 30000)]
+ACGT = b"ACGT"
+
+
+@pytest.mark.parametrize("pxy,pgap", PENALTIES)
+def test_random_vs_oracle_penalties(engine, pxy, pgap):
+    r = random.Random(hash((pxy, pgap)) & 0xffff)
+    genes = _rand_genes(r, 6, 1, 700, ACGT) + _mutants(r, bytes(r.choice(ACGT) for _ in range(650)), 3, ACGT)
+    engine.set_sequences(genes)
+    pen, hs = engine.align_pairs(_all_ids(len(genes)), pxy, pgap)
+    h, opens, ohs = oracle.all_pairs(genes, pxy, pgap)
+    assert [int(v) for v in pen] == opens
+    assert [x.tobytes().hex() for x in hs] == ohs
+
+
+@pytest.mark.parametrize("bits", [4, 8, 16, 32])
+@pytest.mark.parametrize("alpha", [b"ACGT", b"AC", b"ACGTNacgtn_*"])
+def test_forced_widths_and_alphabets(bits, alpha):
+    r = random.Random(bits * 7 + len(alpha))
+    # lengths straddle the 64-column chunk and 512-row band boundaries
+    lens = [1, 2, 63, 64, 65, 511, 512, 513, 1100]
+    genes = [bytes(r.choice(alpha) for _ in range(L)) for L in lens]
+    with seqalign.Engine(device=0, bits=bits) as e:
+        e.set_sequences(genes)
+        pen, hs = e.align_pairs(_all_ids(len(genes)), 3, 2)
+        st = e.stats()
+    assert st["bits"] == bits
+    _, opens, ohs = oracle.all_pairs(genes, 3, 2)
+    assert [int(v) for v in pen] == opens
+    assert [x.tobytes().hex() for x in hs] == ohs
+
+
+def test_subset_and_order_of_pair_ids(engine):
+    r = random.Random(5)
+    genes = _rand_genes(r, 7, 50, 900, ACGT)
+    engine.set_sequences(genes)
+    ids = np.array([20, 3, 0, 17, 9], dtype=np.int64)
+    pen, hs = engine.align_pairs(ids, 3, 2)
+    _, opens, ohs = oracle.all_pairs(genes, 3, 2)
+    assert [int(v) for v in pen] == [opens[i] for i in ids]
+    assert [x.tobytes().hex() for x in hs] == [ohs[i] for i in ids]
+
+
+def test_multi_batch_workspace():
+    """A small HBM budget forces several fill/traceback batches."""
+    r = random.Random(9)
+    genes = _rand_genes(r, 8, 800, 1500, ACGT)
+    with seqalign.Engine(device=0, workspace_bytes=3 << 20) as e:
+        e.set_sequences(genes)
+        pen, hs = e.align_pairs(_all_ids(len(genes)), 3, 2)
+        assert e.stats()["batches"] > 1
+    _, opens, ohs = oracle.all_pairs(genes, 3, 2)
+    assert [int(v) for v in pen] == opens
+    assert [x.tobytes().hex() for x in hs] == ohs
+
+
+@pytest.mark.parametrize("m,n", [(1, 1), (1, 9), (9, 1), (700, 30), (30, 700), (2000, 2100), (3000, 64)])
+def test_single_pair_strings(engine, m, n):
+    r = random.Random(m * 1000 + n)
+    x = bytes(r.choice(ACGT) for _ in range(m))
+    y = bytes(r.choice(ACGT) for _ in range(n))
+    for pxy, pgap in ((3, 2), (5, 1), (-1, 2)):
+        got = engine.get_minimum_penalty(x, y, pxy, pgap)
+        assert got == oracle.pair(x, y, pxy, pgap)
+
+
+def test_get_minimum_penalties_api(golden):
+    c = golden["mseq1"]
+    pxy, pgap, genes = case_input(c)
+    pens = [0] * len(c["penalties"])
+    h = seqalign.getMinimumPenalties(genes, len(genes), pxy, pgap, pens)
+    assert h == c["hash"] and pens == c["penalties"]
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(PKG, "bin", "seqalkway")), reason="driver not built")
+@pytest.mark.parametrize("name", ["mseq", "mseq1", "xulin_test", "k1", "k0"])
+def test_driver_stdout_contract(golden, name):
+    c = golden[name]
+    if "file" in c:
+        text = open(os.path.join(GOLDEN_DIR, "data", c["file"]), "rb").read()
+    else:
+        text = c["input"].encode("latin-1")
+    out = subprocess.run([os.path.join(PKG, "bin", "seqalkway")], input=text, stdout=subprocess.PIPE,
+                         check=True, timeout=300).stdout.decode()
+    lines = out.split("\n")
+    assert lines[0].startswith("Time: ") and lines[0].endswith(" us")
+    assert lines[1] == c["hash"]
+    assert lines[2] == "".join("%d " % p for p in c["penalties"])
+
+
+def test_multi_gpu_allgather_inprocess(golden):
+    if seqalign.device_count() < 2:
+        pytest.skip("needs >= 2 devices for the in-process RCCL path")
+    c = golden["xulin_test"]
+    pxy, pgap, genes = case_input(c)
+    pens = [0] * len(c["penalties"])
+    h = seqalign.getMinimumPenalties(genes, len(genes), pxy, pgap, pens, ngpus=2)
+    assert h == c["hash"] and pens == c["penalties"]
+
+
+def test_sharded_union_equals_unsharded(engine, golden):
+    """Emulated G-way shard: shards run one after another on one GPU."""
+    pxy, pgap, genes = case_input(golden["xulin_test"])
+    engine.set_sequences(genes)
+    lengths = [len(g) for g in genes]
+    P = len(genes) * (len(genes) - 1) // 2
+    pen = np.zeros(P, dtype=np.int32)
+    hs = np.zeros((P, 64), dtype=np.uint8)
+    for r in range(8):
+        ids = seqalign.shard_pairs(lengths, r, 8)
+        p, h = engine.align_pairs(ids, pxy, pgap)
+        pen[ids] = p
+        hs[ids] = h
+    assert seqalign.chain_hash(hs) == golden["xulin_test"]["hash"]
