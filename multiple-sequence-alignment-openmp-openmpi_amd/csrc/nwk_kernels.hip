@@ -212,11 +212,22 @@ __global__ __launch_bounds__(256) void nw_fill(FillArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Traceback (skel:236-262 priority: DIAG on match > DIAG if diag+pxy==H >
-// UP if up+pgap==H > LEFT), one thread per pair, on the stored G mod 2^W.
+// Traceback (skel:236-262 / sub:502-531 priority: DIAG on match > DIAG if
+// diag+pxy==H > UP if up+pgap==H > LEFT) on the stored G mod 2^W.
+//
+// One wave per pair.  The walk itself is sequential and uniform (all lanes
+// run it, so its state lives in SGPRs); the wave's lanes only move data:
+// the stored matrix is staged in LDS one tile at a time -- a band's 512 rows
+// x TC dword columns (+ overlap below) -- by LDS-DMA (global_load_lds_dword),
+// and the next tile down the band is prefetched while the walk runs.  Each
+// step then costs one round of broadcast ds_reads instead of dependent HBM
+// loads.  Ops are emitted reversed, 4 per dword, by lane 0.
 // ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
 template <int W>
-__device__ __forceinline__ unsigned getG(const unsigned* M, const PairDesc& pd, int64_t bdw, int i, int j) {
+__device__ __forceinline__ unsigned getG_global(const unsigned* M, const PairDesc& pd, int64_t bdw, int i, int j) {
   if (i == 0 || j == 0) return 0u;
   constexpr int SPD = 32 / W;
   const int w = i - 1;
@@ -230,36 +241,169 @@ __device__ __forceinline__ unsigned getG(const unsigned* M, const PairDesc& pd, 
   else return (d >> (W * (s % SPD))) & ((1u << W) - 1u);
 }
 
+struct Five { unsigned v[5]; };
+
+template <int W>
+__device__ __noinline__ Five tb_fallback(const unsigned* mat, const PairDesc& pd, int64_t bdw, const uint8_t* xg,
+                                         const uint8_t* yg, int ci, int cj, bool xin, bool yin, bool fg, bool fu,
+                                         bool fd, int shg, int shu, int shd, Five in) {
+  Five o = in;
+  if (!xin && ci >= 1) o.v[0] = xg[ci - 1];
+  if (!yin && cj >= 1) o.v[1] = yg[cj - 1];
+  if (fg) o.v[2] = getG_global<W>(mat, pd, bdw, ci, cj) << shg;
+  if (fu) o.v[3] = getG_global<W>(mat, pd, bdw, ci - 1, cj) << shu;
+  if (fd) o.v[4] = getG_global<W>(mat, pd, bdw, ci - 1, cj - 1) << shd;
+  return o;
+}
+
+typedef __attribute__((address_space(3))) unsigned lds_u32;
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const lds_u32*)p;
+}
+
 template <int W>
 __global__ __launch_bounds__(64) void nw_traceback(TraceArgs a) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= a.npairs) return;
-  const PairDesc pd = a.pairs[p];
+  constexpr int SPD = 32 / W;
+  constexpr int TC = 8;                      // dword columns per tile window
+  constexpr int TS = TC * SPD;               // steps per tile window
+  constexpr int OV = (11 + SPD - 1) / SPD;   // columns kept below the window: a block reaches s-10
+  constexpr int CC = TC + OV;
+  constexpr int TILE = CC * kRows * kWave;
+  constexpr int YLO = 96;                    // y window starts 96 columns below the tile's first step
   constexpr unsigned MASK = W == 32 ? 0xffffffffu : ((1u << (W & 31)) - 1u);
+  static_assert(TS + YLO <= 256, "y window must fit one DMA");
+  __shared__ __attribute__((aligned(16))) unsigned tile[2][TILE];
+  __shared__ __attribute__((aligned(16))) unsigned xs[2][kBandRows / 4];
+  __shared__ __attribute__((aligned(16))) unsigned ys[2][64];
+
+  const int lane = threadIdx.x;
+  const PairDesc pd = a.pairs[blockIdx.x];
   const int64_t bdw = band_dwords(W, pd.sblocks);
-  const uint8_t* x = a.codes + pd.x_off;
-  const uint8_t* y = a.codes + pd.y_off;
+  const int ncols = 64 * pd.sblocks / SPD;
+  const uint8_t* xg = a.codes + pd.x_off;
+  const uint8_t* yg = a.codes + pd.y_off;
+
+  // Stage tile (b, q) into buffer buf by LDS-DMA: dword columns
+  // [TC*q - OV, TC*q + TC), the band's x codes and the y codes of columns
+  // [TS*q - YLO, TS*q - YLO + 256).  Completion = this wave's vmcnt.
+  auto issue = [&](int buf, int b, int q) {
+    const unsigned* src = a.mat + pd.mat_off + (int64_t)b * bdw + lane;
+    for (int cc = 0; cc < CC; ++cc) {
+      const int c = TC * q - OV + cc;
+      if (c < 0 || c >= ncols) continue;
+#pragma unroll
+      for (int r = 0; r < kRows; ++r)
+        __builtin_amdgcn_global_load_lds((gbl_void*)(src + ((int64_t)c * kRows + r) * kWave),
+                                         (lds_void*)&tile[buf][(cc * kRows + r) * kWave], 4, 0, 0);
+    }
+    const unsigned* xsrc = reinterpret_cast<const unsigned*>(xg + (int64_t)b * kBandRows);
+    __builtin_amdgcn_global_load_lds((gbl_void*)(xsrc + lane), (lds_void*)&xs[buf][0], 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void*)(xsrc + 64 + lane), (lds_void*)&xs[buf][64], 4, 0, 0);
+    const unsigned* ysrc = reinterpret_cast<const unsigned*>(yg + (int64_t)TS * q - YLO);
+    __builtin_amdgcn_global_load_lds((gbl_void*)(ysrc + lane), (lds_void*)&ys[buf][0], 4, 0, 0);
+  };
+  // The walk reads LDS only through inline asm, so the compiler does not
+  // make every read wait for the in-flight DMA: this drain is the one wait.
+  auto drain = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+
   uint8_t* ops = a.ops + pd.ops_off;
   int i = pd.m, j = pd.n, L = 0;
+  unsigned opw = 0;
+  int tb = -1, tq = 0, cur = 0, pb = -1, pq = 0;
+  // this lane's cell of the 8x8 block anchored at (i, j): (i - li, j - lj)
+  const int li = lane >> 3, lj = lane & 7;
+
   while (i > 0 && j > 0) {
-    uint8_t op;
-    if (x[i - 1] == y[j - 1]) {
-      op = 'D';
-    } else {
-      const unsigned g = getG<W>(a.mat, pd, bdw, i, j);
-      const unsigned gd = getG<W>(a.mat, pd, bdw, i - 1, j - 1);
-      const unsigned gu = getG<W>(a.mat, pd, bdw, i - 1, j);
-      if (((gd + (unsigned)a.K1 - g) & MASK) == 0u) op = 'D';
-      else if (((gu - g) & MASK) == 0u) op = 'U';
-      else op = 'L';
+    {  // ---- make the tile holding the block current
+      const int w = (i - 1) & (kBandRows - 1);
+      const int b = (i - 1) / kBandRows;
+      const int s = j - 1 + (w >> 3);
+      if (b != tb || s < TS * tq) {
+        const int q = s / TS;
+        drain();
+        if (!(b == pb && q == pq)) {
+          issue(cur ^ 1, b, q);
+          drain();
+        }
+        cur ^= 1;
+        tb = b;
+        tq = q;
+        pb = -1;
+        if (q > 0) {
+          issue(cur ^ 1, b, q - 1);
+          pb = b;
+          pq = q - 1;
+        }
+      }
     }
-    ops[L++] = op;
-    if (op == 'D') { --i; --j; }
-    else if (op == 'U') { --i; }
-    else { --j; }
+    // ---- every lane decides the traceback move of one cell of the block
+    const int ci = i - li, cj = j - lj;
+    const int slo = TS * tq - OV * SPD, shi = TS * tq + TS;
+    const unsigned tbase = lds_addr(&tile[cur][0]);
+    // address of G(ii, jj) in the tile, or ~0u when outside (border / other band / window)
+    auto gaddr = [&](int ii, int jj, int& sh) -> unsigned {
+      if (ii <= 0 || jj <= 0) { sh = -1; return ~0u; }
+      const int ww = ii - 1 - tb * kBandRows;
+      const int tt = ww >> 3, rr = ww & 7, ss = jj - 1 + tt;
+      sh = W * (ss & (SPD - 1));
+      if (ww < 0 || ss < slo || ss >= shi) return ~1u;
+      return tbase + 4u * (unsigned)(((ss / SPD - (TC * tq - OV)) * kRows + rr) * kWave + tt);
+    };
+    int shg, shu, shd;
+    const unsigned ag = gaddr(ci, cj, shg), au = gaddr(ci - 1, cj, shu), ad = gaddr(ci - 1, cj - 1, shd);
+    const int wx = ci - 1 - tb * kBandRows, wy = cj - 1 - (TS * tq - YLO);
+    const bool xin = ci >= 1 && wx >= 0, yin = cj >= 1 && wy >= 0 && wy < 256;
+    const unsigned ax = xin ? lds_addr(&xs[cur][0]) + (unsigned)wx : lds_addr(&xs[cur][0]);
+    const unsigned ay = yin ? lds_addr(&ys[cur][0]) + (unsigned)wy : lds_addr(&ys[cur][0]);
+    const unsigned z = tbase;
+    unsigned vx, vy, vg, vu, vd;
+    asm volatile(
+        "ds_read_u8 %0, %5\n\t"
+        "ds_read_u8 %1, %6\n\t"
+        "ds_read_b32 %2, %7\n\t"
+        "ds_read_b32 %3, %8\n\t"
+        "ds_read_b32 %4, %9\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(vx), "=&v"(vy), "=&v"(vg), "=&v"(vu), "=&v"(vd)
+        : "v"(ax), "v"(ay), "v"(ag < ~1u ? ag : z), "v"(au < ~1u ? au : z), "v"(ad < ~1u ? ad : z)
+        : "memory");
+    // rare: cells of the band above / outside the staged window -> global,
+    // in a non-inlined call so the wait for those loads (which also drains
+    // the tile prefetch) stays on this path.
+    if ((!xin && ci >= 1) || (!yin && cj >= 1) || ag == ~1u || au == ~1u || ad == ~1u) {
+      const Five f = tb_fallback<W>(a.mat, pd, bdw, xg, yg, ci, cj, xin, yin, ag == ~1u, au == ~1u, ad == ~1u,
+                                    shg, shu, shd, Five{vx, vy, vg, vu, vd});
+      vx = f.v[0]; vy = f.v[1]; vg = f.v[2]; vu = f.v[3]; vd = f.v[4];
+    }
+    const unsigned g = ag == ~0u ? 0u : (vg >> shg) & MASK;
+    const unsigned gu = au == ~0u ? 0u : (vu >> shu) & MASK;
+    const unsigned gd = ad == ~0u ? 0u : (vd >> shd) & MASK;
+    const bool isD = (vx & 0xffu) == (vy & 0xffu) || ((gd + (unsigned)a.K1 - g) & MASK) == 0u;
+    const bool isU = !isD && ((gu - g) & MASK) == 0u;
+    const unsigned long long mD = __ballot(isD), mU = __ballot(isU);
+    // ---- sequential walk through the block on the two masks (SALU only)
+    int di = 0, dj = 0;
+    while (di < 8 && dj < 8 && i - di > 0 && j - dj > 0) {
+      const int k = di * 8 + dj;
+      const unsigned op = ((mD >> k) & 1ull) ? 'D' : ((mU >> k) & 1ull) ? 'U' : 'L';
+      opw |= op << (8 * (L & 3));
+      if ((L & 3) == 3) {
+        if (lane == 0) *reinterpret_cast<unsigned*>(ops + (L & ~3)) = opw;
+        opw = 0;
+      }
+      ++L;
+      di += op != 'L';
+      dj += op != 'U';
+    }
+    i -= di;
+    j -= dj;
   }
-  a.oplen[pd.slot] = L;
-  a.endij[pd.slot] = make_int2(i, j);
+  if ((L & 3) != 0 && lane == 0) *reinterpret_cast<unsigned*>(ops + (L & ~3)) = opw;
+  drain();
+  if (lane == 0) {
+    a.oplen[pd.slot] = L;
+    a.endij[pd.slot] = make_int2(i, j);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -309,7 +453,7 @@ int fill_blocks_per_cu(int mode, int bits) {
 }
 
 hipError_t launch_traceback(int bits, const TraceArgs& a, hipStream_t s) {
-  const int grid = (a.npairs + 63) / 64;
+  const int grid = a.npairs;  // one wave per pair
   if (grid == 0) return hipSuccess;
   switch (bits) {
     case 4: hipLaunchKernelGGL((nw_traceback<4>), dim3(grid), dim3(64), 0, s, a); break;

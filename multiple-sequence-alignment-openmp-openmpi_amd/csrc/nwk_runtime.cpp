@@ -203,8 +203,12 @@ int nwk_ctx_create(const nwk_opts* opts, nwk_ctx** out) {
   for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
   size_t fr = 0, tot = 0;
   HIP_TRY(hipMemGetInfo(&fr, &tot));
-  c->budget = o.workspace_bytes > 0 ? o.workspace_bytes : (int64_t)((double)fr * 0.92) - (512ll << 20);
-  if (c->budget < (64ll << 20)) c->budget = 64ll << 20;
+  if (o.workspace_bytes > 0) {
+    c->budget = o.workspace_bytes;
+  } else {
+    c->budget = (int64_t)((double)fr * 0.92) - (512ll << 20);
+    if (c->budget < (64ll << 20)) c->budget = 64ll << 20;
+  }
   unsigned hc = std::thread::hardware_concurrency();
   c->host_threads = o.host_threads > 0 ? o.host_threads : (int)std::min(16u, hc ? hc : 1u);
   HIP_TRY(c->d_ctl.ensure(256) == NWK_OK ? hipSuccess : hipErrorOutOfMemory);
@@ -234,7 +238,7 @@ int nwk_set_sequences(nwk_ctx* c, const uint8_t* seqs, const int64_t* offsets, i
   // layout: codes 8-aligned; E with kEPad entries before column 0 and 256 after the end
   c->c_off.resize(k);
   c->e_off.resize(k);
-  int64_t co = 0, eo = 0;
+  int64_t co = 64, eo = 0;  // codes: 64-byte front pad (traceback y windows start 64 before)
   for (int s = 0; s < k; ++s) {
     const int64_t L = c->off[s + 1] - c->off[s];
     c->c_off[s] = co;
@@ -255,7 +259,8 @@ namespace {
 int build_encoding(nwk_ctx* c, int kind) {
   if (c->built[kind]) return NWK_OK;
   const int k = c->k;
-  const int64_t ncodes = k ? c->c_off[k - 1] + round_up(c->off[k] - c->off[k - 1] + 8, 8) : 8;
+  // + 512-byte tail pad: the traceback stages whole 512-row x windows and 256-byte y windows
+  const int64_t ncodes = (k ? c->c_off[k - 1] + round_up(c->off[k] - c->off[k - 1] + 8, 8) : 64) + 512;
   const int64_t nE = k ? c->e_off[k - 1] - kEPad + kEPad + (c->off[k] - c->off[k - 1]) + 256 : 64;
   std::vector<uint8_t> codes((size_t)ncodes, 0);
   std::vector<uint32_t> E((size_t)nE, 0);

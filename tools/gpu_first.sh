@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 echo "== smoke"; timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tee gpurun_out/smoke.log
-echo "== pytest gpu"; timeout -k 10 540 python -m pytest tests/ -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 || { tail -50 gpurun_out/pytest_gpu.log; exit 1; }
+echo "== pytest gpu"; timeout -k 10 540 python -m pytest tests/ -q -m gpu --durations=15 > gpurun_out/pytest_gpu.log 2>&1 || { tail -50 gpurun_out/pytest_gpu.log; exit 1; }
 tail -3 gpurun_out/pytest_gpu.log
 echo "== bench"; timeout -k 10 200 python bench.py --steps 3 --warmup 1 --verbose > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -30 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
