@@ -37,30 +37,23 @@ struct FillArgs {
   const PairDesc* pairs;
   const int2* tasks;       // {pair index, band}, dependency-ordered
   int ntasks;
-  const uint8_t* codes;    // sequence codes (x rows)
+  const uint8_t* codes;    // sequence codes (x rows, y columns)
   const uint32_t* E;       // expanded column codes, 4 per dword
   uint32_t* mat;           // packed G = H - (i+j)*pgap, W bits per cell
   unsigned long long* bnd; // {epoch:32 | G:32} granules, one per boundary cell
   unsigned* counter;       // task dequeue head
   unsigned* err;           // nonzero = a hand-off timed out
+  unsigned* done;          // per slot: bands finished (released at agent scope)
+  uint8_t* ops;            // per pair, reversed traceback moves: 'D','U','L'
+  int* oplen;              // per slot
+  int2* endij;             // per slot: (i, j) where the traced walk stopped
+  unsigned long long* stamps;  // optional (verbose >= 2): per slot {fill done, traced}, s_memrealtime
   unsigned epoch;
   int K0, K1;              // diag increments in G-space: match, mismatch
 };
 
-struct TraceArgs {
-  const PairDesc* pairs;
-  int npairs;
-  const uint8_t* codes;
-  const uint32_t* mat;
-  uint8_t* ops;            // per pair, reversed: 'D','U','L'
-  int* oplen;              // per slot
-  int2* endij;             // per slot: (i, j) where the traced walk stopped
-  int K1;
-};
-
 // Launchers (nwk_kernels.hip).  bits in {4, 8, 16, 32}.
 hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStream_t s);
-hipError_t launch_traceback(int bits, const TraceArgs& a, hipStream_t s);
 int fill_blocks_per_cu(int mode, int bits);
 
 // Dwords of one band of the stored matrix.

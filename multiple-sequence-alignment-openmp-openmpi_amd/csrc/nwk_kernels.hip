@@ -44,6 +44,42 @@ __device__ __forceinline__ void st_granule(u64* p, unsigned epoch, int v) {
   __hip_atomic_store((gu64*)p, ((u64)epoch << 32) | (unsigned)v, RLX_AGENT);
 }
 
+// Loads the compiler does not track.  The block loop issues its prefetch
+// loads here and waits for them itself with a COUNTED s_waitcnt right after
+// the block's stores (vmcnt counts loads and stores together, in order): the
+// compiler's own loop-header vmcnt(0) would otherwise make every block wait
+// for the previous block's HBM stores to complete.
+__device__ __forceinline__ void asm_load_E(const unsigned* p, unsigned& e0, unsigned& e1) {
+  asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %2, off offset:16"
+               : "=&v"(e0), "=&v"(e1)
+               : "v"(p)
+               : "memory");
+}
+__device__ __forceinline__ void asm_load_granule(const u64* p, u64& v) {
+  asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=&v"(v) : "v"(p) : "memory");
+}
+// Waits until at most N vector-memory ops are outstanding; the "+v" operands
+// order every later use of those registers after the wait.
+template <int N>
+__device__ __forceinline__ void wait_vm_keep(unsigned& a, unsigned& b, u64& c) {
+  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "n"(N) : "memory");
+}
+
+// A zero the optimiser cannot see: LLVM rewrites an idempotent atomic RMW
+// (add 0) into a plain atomic load, which can be served by a stale copy in
+// this XCD's L2.  A real RMW is performed at the coherence point.
+__device__ __forceinline__ unsigned long long opaque_zero64() {
+  unsigned long long z = 0;
+  asm volatile("" : "+v"(z));
+  return z;
+}
+__device__ __forceinline__ unsigned opaque_zero32() {
+  unsigned z = 0;
+  asm volatile("" : "+v"(z));
+  return z;
+}
+
 // Polls until every lane's granule carries `epoch` and returns it.  Bounded:
 // gives up after ~4 s of wall time (s_memrealtime runs at 100 MHz) or when
 // another wave has already failed, so a hand-off bug ends the grid instead of
@@ -58,7 +94,11 @@ __device__ __noinline__ u64 wait_granules(const u64* p, unsigned epoch, u64 v, u
       if ((threadIdx.x & 63) == 0) atomicOr(err, 1u);
       return 0;
     }
-    v = ld_granule(p);
+    // Re-read through an atomic: it is performed at the coherence point, so a
+    // stale copy of the line in this XCD's L2 (left by the first, too-early
+    // load) cannot keep the poll spinning.  The tag makes any copy safe to
+    // USE; only liveness needs the coherent re-read.
+    v = __hip_atomic_fetch_add((gu64*)p, opaque_zero64(), RLX_AGENT);
   }
 }
 
@@ -124,12 +164,295 @@ __device__ __forceinline__ void step_block(int s0, int lane, int (&h)[kRows], in
   }
 }
 
+// ---------------------------------------------------------------------------
+// Traceback (skel:236-262 / sub:502-531 priority: DIAG on match > DIAG if
+// diag+pxy==H > UP if up+pgap==H > LEFT) on the stored G mod 2^W.
+//
+// Fused into the fill kernel: the wave that finishes a pair's last band
+// (told by the pair's band counter, after every band wave released its
+// stores) traces that pair, while the other waves keep filling later pairs.
+// Per 8x8 block of cells anchored at the current cell, every lane decides
+// the move of one cell (one round of LDS reads), two ballots give the D and
+// U masks, and the sequential walk through the block runs on those masks in
+// scalar code.  The matrix is staged in LDS by LDS-DMA one tile at a time:
+// 16 lanes x 8 rows of one band x TC dword columns (+ overlap below), with
+// the next tile down the band prefetched.  Ops are emitted reversed, 4 per
+// dword, by lane 0.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+typedef __attribute__((address_space(3))) unsigned lds_u32;
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const lds_u32*)p;
+}
+
+template <int W>
+struct TbConf {
+  static constexpr int SPD = 32 / W;
+  static constexpr int TC = 8;                      // dword columns per window
+  static constexpr int TS = TC * SPD;               // steps per window
+  static constexpr int OV = (11 + SPD - 1) / SPD;   // columns below: a block reaches s-10
+  static constexpr int CC = TC + OV;
+  static constexpr int TL = 16;                     // lanes (8-row groups) per tile
+  static constexpr int TILE = CC * kRows * TL;      // dwords
+  static constexpr int NB = W <= 8 ? 2 : 1;         // double-buffered where LDS allows
+  static constexpr int YLO = 96;                    // y window starts 96 columns below the window
+  static_assert(TILE % 64 == 0, "tile = whole DMA instructions");
+  static_assert(TS + YLO <= 256, "y window must fit one DMA");
+};
+
+template <int W>
+struct TbLds {
+  unsigned tile[TbConf<W>::NB][TbConf<W>::TILE];
+  unsigned xs[TbConf<W>::NB][64];
+  unsigned ys[TbConf<W>::NB][64];
+  unsigned obuf[64];   // 256-byte ring of traceback moves, flushed to HBM in dwords
+};
+
+template <int W>
+__device__ __forceinline__ unsigned getG_global(const unsigned* M, const PairDesc& pd, int64_t bdw, int i, int j) {
+  if (i == 0 || j == 0) return 0u;
+  constexpr int SPD = 32 / W;
+  const int w = i - 1;
+  const int b = w / kBandRows;
+  const int wr = w - b * kBandRows;
+  const int t = wr / kRows;
+  const int r = wr - t * kRows;
+  const int s = j - 1 + t;
+  const unsigned d = M[pd.mat_off + (int64_t)b * bdw + ((int64_t)(s / SPD) * kRows + r) * kWave + t];
+  if constexpr (W == 32) return d;
+  else return (d >> (W * (s % SPD))) & ((1u << W) - 1u);
+}
+
+struct Five { unsigned v[5]; };
+
+// Rare cells (band above, outside the staged window) come from global memory
+// in a non-inlined call, so the wait for those loads -- which also drains the
+// tile prefetch -- stays on this path.
+template <int W>
+__device__ __noinline__ Five tb_fallback(const unsigned* mat, const PairDesc& pd, int64_t bdw, const uint8_t* xg,
+                                         const uint8_t* yg, int ci, int cj, bool fx, bool fy, bool fg, bool fu,
+                                         bool fd, int shg, int shu, int shd, Five in) {
+  Five o = in;
+  if (fx) o.v[0] = xg[ci - 1];
+  if (fy) o.v[1] = yg[cj - 1];
+  if (fg) o.v[2] = getG_global<W>(mat, pd, bdw, ci, cj) << shg;
+  if (fu) o.v[3] = getG_global<W>(mat, pd, bdw, ci - 1, cj) << shu;
+  if (fd) o.v[4] = getG_global<W>(mat, pd, bdw, ci - 1, cj - 1) << shd;
+  return o;
+}
+
+template <int W>
+__device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd, TbLds<W>& L, int lane) {
+  using C = TbConf<W>;
+  constexpr int SPD = C::SPD;
+  constexpr int LSPD = SPD == 8 ? 3 : SPD == 4 ? 2 : SPD == 2 ? 1 : 0;
+  constexpr unsigned MASK = W == 32 ? 0xffffffffu : ((1u << (W & 31)) - 1u);
+  const int64_t bdw = band_dwords(W, pd.sblocks);
+  const int ncols = 64 * pd.sblocks / SPD;
+  const uint8_t* xg = a.codes + pd.x_off;
+  const uint8_t* yg = a.codes + pd.y_off;
+  const unsigned* mb = a.mat + pd.mat_off;
+  const bool prof = a.stamps != nullptr;
+  unsigned long long cy_sw = 0, cy_blk = 0, n_blk = 0, n_sw = 0, n_sync = 0, n_slow = 0, tA = 0, tB;
+
+  // Stage tile (b, q, t0) into buffer buf by LDS-DMA: lanes [t0, t0+16) of
+  // band b, dword columns [TC*q - OV, TC*q + TC) (clamped), the x codes of
+  // rows [512b + 8t0, +256) and the y codes of columns [TS*q - YLO, +256).
+  // DMA k covers column k/2, rows 4(k&1) + lane/16, lanes t0 + lane%16.
+  const int lane_off = (lane >> 4) * kWave + (lane & 15);
+  auto issue = [&](int buf, int b, int q, int t0) {
+    const unsigned* src = mb + (int64_t)b * bdw + t0 + lane_off;
+#pragma unroll
+    for (int k = 0; k < C::TILE / 64; ++k) {
+      int c = C::TC * q - C::OV + (k >> 1);
+      c = c < 0 ? 0 : (c >= ncols ? ncols - 1 : c);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (int64_t)c * (kRows * kWave) + (k & 1) * 4 * kWave),
+                                       (lds_void*)&L.tile[buf][64 * k], 4, 0, 0);
+    }
+    const unsigned* xsrc = reinterpret_cast<const unsigned*>(xg + (int64_t)b * kBandRows + 8 * t0);
+    __builtin_amdgcn_global_load_lds((gbl_void*)(xsrc + lane), (lds_void*)&L.xs[buf][0], 4, 0, 0);
+    const unsigned* ysrc = reinterpret_cast<const unsigned*>(yg + (int64_t)C::TS * q - C::YLO);
+    __builtin_amdgcn_global_load_lds((gbl_void*)(ysrc + lane), (lds_void*)&L.ys[buf][0], 4, 0, 0);
+  };
+  // The walk reads LDS only through inline asm, so the compiler does not
+  // make every read wait for the in-flight DMA: this drain is the one wait.
+  auto drain = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+
+  uint8_t* ops = a.ops + pd.ops_off;
+  int i = pd.m, j = pd.n, Lc = 0, flushed = 0;
+  int tb = -1, tq = 0, tt0 = 0, cur = 0, pb = -1, pq = 0, pt0 = 0;
+  const unsigned ob = lds_addr(&L.obuf[0]);
+  // Moves go to an LDS ring (ds_write_b8, no VMEM) and reach HBM as whole
+  // dwords: a store in flight would otherwise make every drain() wait for it.
+  auto flush = [&](int upto) {  // copy ring bytes [flushed, upto) (upto % 4 == 0 or final)
+    const int from = flushed & ~3;
+    for (int o = from + 4 * lane; o < upto; o += 256) {  // one pass: upto - from <= 256
+      unsigned v;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ob + (unsigned)(o & 255)) : "memory");
+      *reinterpret_cast<unsigned*>(ops + o) = v;
+    }
+    flushed = upto;
+  };
+  const int li = lane >> 3, lj = lane & 7;  // this lane's cell: (i - li, j - lj)
+
+  while (i > 0 && j > 0) {
+    if (prof) tA = __builtin_amdgcn_s_memtime();
+    const int w = (i - 1) & (kBandRows - 1);
+    const int t = w >> 3;
+    {  // ---- make the tile holding the 8x8 block at (i, j) current
+      const int b = (i - 1) / kBandRows;
+      const int tl = t > 0 ? t - 1 : 0;  // lowest lane of this band the block touches
+      const int s = j - 1 + t;
+      if (b != tb || s < C::TS * tq || tl < tt0 || t >= tt0 + C::TL) {
+        const int q = s / C::TS;
+        drain();
+        n_sw++;
+        flush(Lc & ~3);  // stores issued right after a drain have a whole tile to land
+        if (C::NB == 2 && b == pb && q == pq && tl >= pt0 && t < pt0 + C::TL) {
+          cur ^= 1;
+          tt0 = pt0;
+        } else {
+          n_sync++;
+          const int nt0 = max(0, t - (C::TL - 3));
+          const int nbuf = C::NB == 2 ? (cur ^ 1) : 0;
+          issue(nbuf, b, q, nt0);
+          drain();
+          cur = nbuf;
+          tt0 = nt0;
+        }
+        tb = b;
+        tq = q;
+        pb = -1;
+        if (C::NB == 2 && q > 0) {  // the walk moves down the band: prefetch the next window
+          pt0 = max(0, t - (C::TL - 1));
+          issue(cur ^ 1, b, q - 1, pt0);
+          pb = b;
+          pq = q - 1;
+        }
+      }
+    }
+    if (prof) { tB = __builtin_amdgcn_s_memtime(); cy_sw += tB - tA; tA = tB; }
+    n_blk++;
+    const int cbase = C::TC * tq - C::OV;
+    const unsigned tbase = lds_addr(&L.tile[cur][0]);
+    const unsigned xb = lds_addr(&L.xs[cur][0]), yb = lds_addr(&L.ys[cur][0]);
+    unsigned vx, vy, vg, vu, vd;
+    int shg, shu, shd;
+    bool bg, bu, bd;  // border cells (G = 0)
+    // Fast path (uniform test): the block and its up/diag neighbours lie in
+    // this band, inside the staged window and off the border -> branch-free.
+    if (w >= 8 && j >= 9) {
+      const int wc = w - li, wu = wc - 1;
+      const int tc = wc >> 3, rc = wc & 7, tu = wu >> 3, ru = wu & 7;
+      const int jc = j - 1 - lj;  // 0-based column of the cell
+      const int sc = jc + tc, su = jc + tu, sd = su - 1;
+      const unsigned ag = tbase + 4u * (unsigned)((((sc >> LSPD) - cbase) * kRows + rc) * C::TL + tc - tt0);
+      const unsigned au = tbase + 4u * (unsigned)((((su >> LSPD) - cbase) * kRows + ru) * C::TL + tu - tt0);
+      const unsigned ad = tbase + 4u * (unsigned)((((sd >> LSPD) - cbase) * kRows + ru) * C::TL + tu - tt0);
+      shg = W == 32 ? 0 : W * (sc & (SPD - 1));
+      shu = W == 32 ? 0 : W * (su & (SPD - 1));
+      shd = W == 32 ? 0 : W * (sd & (SPD - 1));
+      const unsigned ax = xb + (unsigned)(wc - 8 * tt0);
+      const unsigned ay = yb + (unsigned)(jc - (C::TS * tq - C::YLO));
+      asm volatile(
+          "ds_read_u8 %0, %5\n\t"
+          "ds_read_u8 %1, %6\n\t"
+          "ds_read_b32 %2, %7\n\t"
+          "ds_read_b32 %3, %8\n\t"
+          "ds_read_b32 %4, %9\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(vx), "=&v"(vy), "=&v"(vg), "=&v"(vu), "=&v"(vd)
+          : "v"(ax), "v"(ay), "v"(ag), "v"(au), "v"(ad)
+          : "memory");
+      bg = bu = bd = false;
+    } else {  // slow path: band top, border, or outside the window
+      n_slow++;
+      const int ci = i - li, cj = j - lj;
+      const int slo = C::TS * tq - C::OV * SPD, shi = C::TS * tq + C::TS;
+      // LDS address of G(ii, jj), ~0u on the border (G = 0), ~1u if not staged
+      auto gaddr = [&](int ii, int jj, int& sh) -> unsigned {
+        if (ii <= 0 || jj <= 0) { sh = 0; return ~0u; }
+        const int ww = ii - 1 - tb * kBandRows;
+        const int tt = ww >> 3, rr = ww & 7, ss = jj - 1 + tt;
+        sh = W == 32 ? 0 : W * (ss & (SPD - 1));
+        if (ww < 0 || tt < tt0 || tt >= tt0 + C::TL || ss < slo || ss >= shi) return ~1u;
+        return tbase + 4u * (unsigned)(((ss / SPD - cbase) * kRows + rr) * C::TL + (tt - tt0));
+      };
+      const unsigned ag = gaddr(ci, cj, shg), au = gaddr(ci - 1, cj, shu), ad = gaddr(ci - 1, cj - 1, shd);
+      const int wx = ci - 1 - (tb * kBandRows + 8 * tt0), wy = cj - 1 - (C::TS * tq - C::YLO);
+      const bool xin = ci >= 1 && wx >= 0 && wx < 256, yin = cj >= 1 && wy >= 0 && wy < 256;
+      const unsigned ax = xin ? xb + (unsigned)wx : xb;
+      const unsigned ay = yin ? yb + (unsigned)wy : yb;
+      asm volatile(
+          "ds_read_u8 %0, %5\n\t"
+          "ds_read_u8 %1, %6\n\t"
+          "ds_read_b32 %2, %7\n\t"
+          "ds_read_b32 %3, %8\n\t"
+          "ds_read_b32 %4, %9\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(vx), "=&v"(vy), "=&v"(vg), "=&v"(vu), "=&v"(vd)
+          : "v"(ax), "v"(ay), "v"(ag < ~1u ? ag : tbase), "v"(au < ~1u ? au : tbase), "v"(ad < ~1u ? ad : tbase)
+          : "memory");
+      const bool fx = !xin && ci >= 1, fy = !yin && cj >= 1;
+      if (fx || fy || ag == ~1u || au == ~1u || ad == ~1u) {
+        const Five f = tb_fallback<W>(a.mat, pd, bdw, xg, yg, ci, cj, fx, fy, ag == ~1u, au == ~1u, ad == ~1u, shg,
+                                      shu, shd, Five{vx, vy, vg, vu, vd});
+        vx = f.v[0]; vy = f.v[1]; vg = f.v[2]; vu = f.v[3]; vd = f.v[4];
+      }
+      bg = ag == ~0u;
+      bu = au == ~0u;
+      bd = ad == ~0u;
+    }
+    const unsigned g = bg ? 0u : (vg >> shg) & MASK;
+    const unsigned gu = bu ? 0u : (vu >> shu) & MASK;
+    const unsigned gd = bd ? 0u : (vd >> shd) & MASK;
+    const bool isD = (vx & 0xffu) == (vy & 0xffu) || ((gd + (unsigned)a.K1 - g) & MASK) == 0u;
+    const bool isU = !isD && ((gu - g) & MASK) == 0u;
+    // ---- the walk: each lane packs its cell's move (ASCII) and successor
+    // lane (64 = leaves the block or reaches the border); the walk is a chain
+    // of v_readlane with a scalar lane index, one uniform byte store per step.
+    const int nli = li + (isD || isU ? 1 : 0), nlj = lj + (isU ? 0 : 1);
+    const bool leaves = nli > 7 || nlj > 7 || i - nli <= 0 || j - nlj <= 0;
+    const unsigned code = ((isD ? (unsigned)'D' : isU ? (unsigned)'U' : (unsigned)'L') << 8) |
+                          (leaves ? 64u : (unsigned)(nli * 8 + nlj));
+    unsigned curl = 0, last = 0, cw = 0;
+    do {
+      last = curl;
+      cw = __builtin_amdgcn_readlane(code, curl);
+      asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(cw >> 8) : "memory");
+      ++Lc;
+      curl = cw & 0xffu;
+    } while (curl < 64u);
+    if (Lc - flushed >= 160) flush(Lc & ~3);  // ring of 256, a block adds <= 15: never overrun
+    // the last cell visited and its move give the block's total displacement
+    const unsigned op = cw >> 8;
+    i -= (int)(last >> 3) + (op != 'L' ? 1 : 0);
+    j -= (int)(last & 7u) + (op != 'U' ? 1 : 0);
+    if (prof) { tB = __builtin_amdgcn_s_memtime(); cy_blk += tB - tA; }
+  }
+  if (prof && lane == 0) {
+    unsigned long long* st = a.stamps + 8 * pd.slot + 2;
+    st[0] = cy_sw; st[1] = n_slow; st[2] = cy_blk; st[3] = n_blk; st[4] = n_sw; st[5] = n_sync;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  flush(Lc);
+  drain();
+  if (lane == 0) {
+    a.oplen[pd.slot] = Lc;
+    a.endij[pd.slot] = make_int2(i, j);
+  }
+}
+
 template <int MODE, int W>
-__global__ __launch_bounds__(256) void nw_fill(FillArgs a) {
+__global__ __launch_bounds__(256) void nw_align(FillArgs a) {
   constexpr int SPD = 32 / W;
   __shared__ __attribute__((aligned(16))) int ring_all[4][128];
+  __shared__ __attribute__((aligned(16))) TbLds<W> tbl[4];
   const int lane = threadIdx.x & 63;
-  int* ring = ring_all[threadIdx.x >> 6];
+  const int wid = threadIdx.x >> 6;
+  int* ring = ring_all[wid];
 
   for (;;) {
     unsigned tk = 0;
@@ -161,7 +484,10 @@ __global__ __launch_bounds__(256) void nw_fill(FillArgs a) {
     const bool from_above = band > 0;
     const bool to_below = band + 1 < pd.nbands;
     const int64_t bstride = (int64_t)pd.nchunks * 64;
-    const u64* gin = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)(band - 1) * bstride + lane;
+    // band 0 has no band above: its (never checked) prefetches read the
+    // pair's own boundary area, which is always inside the workspace
+    const u64* gin = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)(band > 0 ? band - 1 : 0) * bstride + lane;
+    const int last_chunk = pd.nchunks > 0 ? pd.nchunks - 1 : 0;
     u64* gout = a.bnd + pd.bnd_off + (int64_t)band * bstride + lane;
     const unsigned* Ep = a.E + pd.e_off - lane;
     unsigned* mptr = a.mat + pd.mat_off + (int64_t)band * band_dwords(W, pd.sblocks) + lane;
@@ -172,9 +498,13 @@ __global__ __launch_bounds__(256) void nw_fill(FillArgs a) {
     for (int r = 0; r < kRows; ++r) { h[r] = 0; acc[r] = 0; }
     int Up = 0, stage = 0;
     u64 pend = 0;
-    if (from_above && pd.nchunks > 0) pend = ld_granule(gin);
-    unsigned e0 = Ep[0], e1 = Ep[4];
+    unsigned e0, e1;
+    asm_load_E(Ep, e0, e1);
+    asm_load_granule(gin, pend);
+    wait_vm_keep<0>(e0, e1, pend);
     bool ok = true;
+    // stores one block issues after its prefetch loads (<= 63: vmcnt field)
+    constexpr int kBlockStores = (8 / SPD) * kRows > 63 ? 63 : (8 / SPD) * kRows;
 
     for (int sb = 0; sb < pd.sblocks; ++sb) {
       // --- band-above row for this super-block: B[64sb+1 .. 64sb+64] = chunk sb+1
@@ -185,8 +515,10 @@ __global__ __launch_bounds__(256) void nw_fill(FillArgs a) {
           if (!__all((unsigned)(pend >> 32) == a.epoch)) { ok = false; break; }
         }
         bval = (int)(unsigned)pend;
-        if (sb + 1 < pd.nchunks) pend = ld_granule(gin + 64 * (sb + 1));
       }
+      // prefetch chunk sb+2 (unconditional, clamped: no control flow between
+      // this load and the counted wait at the end of block 0 that covers it)
+      asm_load_granule(gin + 64 * min(sb + 1, last_chunk), pend);
       int* slot = ring + (sb & 1) * 64;
       slot[lane] = bval;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -194,12 +526,16 @@ __global__ __launch_bounds__(256) void nw_fill(FillArgs a) {
 
       for (int blk = 0; blk < 8; ++blk) {
         const int s0 = sb * 64 + blk * 8;
-        const unsigned ne0 = Ep[s0 + 8], ne1 = Ep[s0 + 12];  // next block's columns
+        unsigned ne0, ne1;
+        asm_load_E(Ep + s0 + 8, ne0, ne1);  // next block's columns
         if (sb == 0)
           step_block<MODE, W, true>(s0, lane, h, Up, stage, acc, xq, e0, e1, slot + blk * 8, mptr, a.K0, a.K1);
         else
           step_block<MODE, W, false>(s0, lane, h, Up, stage, acc, xq, e0, e1, slot + blk * 8, mptr, a.K0, a.K1);
         mptr += (8 / SPD) * kRows * kWave;
+        // the prefetch (and the granule issued before it) are older than the
+        // block's kBlockStores stores: waiting for the rest leaves those in flight
+        wait_vm_keep<kBlockStores>(ne0, ne1, pend);
         e0 = ne0;
         e1 = ne1;
       }
@@ -208,208 +544,31 @@ __global__ __launch_bounds__(256) void nw_fill(FillArgs a) {
       __builtin_amdgcn_wave_barrier();
     }
     if (!ok) return;
+    // --- band finished: make its stores visible at agent scope, then count
+    // it (MI355X_MICROARCH.md R1: drain -> release fence -> drain -> counter).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add((gu32*)(a.done + pd.slot), 1u, RLX_AGENT);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    // --- the pair's last band: every band wave has released, so acquire and
+    // trace the pair here while the other waves keep filling.
+    if (prev + 1u == (unsigned)pd.nbands) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
+      trace_pair<W>(a, pd, tbl[wid], lane);
+      if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
+    }
   }
 }
 
-// ---------------------------------------------------------------------------
-// Traceback (skel:236-262 / sub:502-531 priority: DIAG on match > DIAG if
-// diag+pxy==H > UP if up+pgap==H > LEFT) on the stored G mod 2^W.
-//
-// One wave per pair.  The walk itself is sequential and uniform (all lanes
-// run it, so its state lives in SGPRs); the wave's lanes only move data:
-// the stored matrix is staged in LDS one tile at a time -- a band's 512 rows
-// x TC dword columns (+ overlap below) -- by LDS-DMA (global_load_lds_dword),
-// and the next tile down the band is prefetched while the walk runs.  Each
-// step then costs one round of broadcast ds_reads instead of dependent HBM
-// loads.  Ops are emitted reversed, 4 per dword, by lane 0.
-// ---------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) void lds_void;
-typedef const __attribute__((address_space(1))) void gbl_void;
-
-template <int W>
-__device__ __forceinline__ unsigned getG_global(const unsigned* M, const PairDesc& pd, int64_t bdw, int i, int j) {
-  if (i == 0 || j == 0) return 0u;
-  constexpr int SPD = 32 / W;
-  const int w = i - 1;
-  const int b = w / kBandRows;
-  const int wr = w - b * kBandRows;
-  const int t = wr / kRows;
-  const int r = wr - t * kRows;
-  const int s = j - 1 + t;
-  const unsigned d = M[pd.mat_off + (int64_t)b * bdw + ((int64_t)(s / SPD) * kRows + r) * kWave + t];
-  if constexpr (W == 32) return d;
-  else return (d >> (W * (s % SPD))) & ((1u << W) - 1u);
-}
-
-struct Five { unsigned v[5]; };
-
-template <int W>
-__device__ __noinline__ Five tb_fallback(const unsigned* mat, const PairDesc& pd, int64_t bdw, const uint8_t* xg,
-                                         const uint8_t* yg, int ci, int cj, bool xin, bool yin, bool fg, bool fu,
-                                         bool fd, int shg, int shu, int shd, Five in) {
-  Five o = in;
-  if (!xin && ci >= 1) o.v[0] = xg[ci - 1];
-  if (!yin && cj >= 1) o.v[1] = yg[cj - 1];
-  if (fg) o.v[2] = getG_global<W>(mat, pd, bdw, ci, cj) << shg;
-  if (fu) o.v[3] = getG_global<W>(mat, pd, bdw, ci - 1, cj) << shu;
-  if (fd) o.v[4] = getG_global<W>(mat, pd, bdw, ci - 1, cj - 1) << shd;
-  return o;
-}
-
-typedef __attribute__((address_space(3))) unsigned lds_u32;
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-  return (unsigned)(uintptr_t)(const lds_u32*)p;
-}
-
-template <int W>
-__global__ __launch_bounds__(64) void nw_traceback(TraceArgs a) {
-  constexpr int SPD = 32 / W;
-  constexpr int TC = 8;                      // dword columns per tile window
-  constexpr int TS = TC * SPD;               // steps per tile window
-  constexpr int OV = (11 + SPD - 1) / SPD;   // columns kept below the window: a block reaches s-10
-  constexpr int CC = TC + OV;
-  constexpr int TILE = CC * kRows * kWave;
-  constexpr int YLO = 96;                    // y window starts 96 columns below the tile's first step
-  constexpr unsigned MASK = W == 32 ? 0xffffffffu : ((1u << (W & 31)) - 1u);
-  static_assert(TS + YLO <= 256, "y window must fit one DMA");
-  __shared__ __attribute__((aligned(16))) unsigned tile[2][TILE];
-  __shared__ __attribute__((aligned(16))) unsigned xs[2][kBandRows / 4];
-  __shared__ __attribute__((aligned(16))) unsigned ys[2][64];
-
-  const int lane = threadIdx.x;
-  const PairDesc pd = a.pairs[blockIdx.x];
-  const int64_t bdw = band_dwords(W, pd.sblocks);
-  const int ncols = 64 * pd.sblocks / SPD;
-  const uint8_t* xg = a.codes + pd.x_off;
-  const uint8_t* yg = a.codes + pd.y_off;
-
-  // Stage tile (b, q) into buffer buf by LDS-DMA: dword columns
-  // [TC*q - OV, TC*q + TC), the band's x codes and the y codes of columns
-  // [TS*q - YLO, TS*q - YLO + 256).  Completion = this wave's vmcnt.
-  auto issue = [&](int buf, int b, int q) {
-    const unsigned* src = a.mat + pd.mat_off + (int64_t)b * bdw + lane;
-    for (int cc = 0; cc < CC; ++cc) {
-      const int c = TC * q - OV + cc;
-      if (c < 0 || c >= ncols) continue;
-#pragma unroll
-      for (int r = 0; r < kRows; ++r)
-        __builtin_amdgcn_global_load_lds((gbl_void*)(src + ((int64_t)c * kRows + r) * kWave),
-                                         (lds_void*)&tile[buf][(cc * kRows + r) * kWave], 4, 0, 0);
-    }
-    const unsigned* xsrc = reinterpret_cast<const unsigned*>(xg + (int64_t)b * kBandRows);
-    __builtin_amdgcn_global_load_lds((gbl_void*)(xsrc + lane), (lds_void*)&xs[buf][0], 4, 0, 0);
-    __builtin_amdgcn_global_load_lds((gbl_void*)(xsrc + 64 + lane), (lds_void*)&xs[buf][64], 4, 0, 0);
-    const unsigned* ysrc = reinterpret_cast<const unsigned*>(yg + (int64_t)TS * q - YLO);
-    __builtin_amdgcn_global_load_lds((gbl_void*)(ysrc + lane), (lds_void*)&ys[buf][0], 4, 0, 0);
-  };
-  // The walk reads LDS only through inline asm, so the compiler does not
-  // make every read wait for the in-flight DMA: this drain is the one wait.
-  auto drain = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
-
-  uint8_t* ops = a.ops + pd.ops_off;
-  int i = pd.m, j = pd.n, L = 0;
-  unsigned opw = 0;
-  int tb = -1, tq = 0, cur = 0, pb = -1, pq = 0;
-  // this lane's cell of the 8x8 block anchored at (i, j): (i - li, j - lj)
-  const int li = lane >> 3, lj = lane & 7;
-
-  while (i > 0 && j > 0) {
-    {  // ---- make the tile holding the block current
-      const int w = (i - 1) & (kBandRows - 1);
-      const int b = (i - 1) / kBandRows;
-      const int s = j - 1 + (w >> 3);
-      if (b != tb || s < TS * tq) {
-        const int q = s / TS;
-        drain();
-        if (!(b == pb && q == pq)) {
-          issue(cur ^ 1, b, q);
-          drain();
-        }
-        cur ^= 1;
-        tb = b;
-        tq = q;
-        pb = -1;
-        if (q > 0) {
-          issue(cur ^ 1, b, q - 1);
-          pb = b;
-          pq = q - 1;
-        }
-      }
-    }
-    // ---- every lane decides the traceback move of one cell of the block
-    const int ci = i - li, cj = j - lj;
-    const int slo = TS * tq - OV * SPD, shi = TS * tq + TS;
-    const unsigned tbase = lds_addr(&tile[cur][0]);
-    // address of G(ii, jj) in the tile, or ~0u when outside (border / other band / window)
-    auto gaddr = [&](int ii, int jj, int& sh) -> unsigned {
-      if (ii <= 0 || jj <= 0) { sh = -1; return ~0u; }
-      const int ww = ii - 1 - tb * kBandRows;
-      const int tt = ww >> 3, rr = ww & 7, ss = jj - 1 + tt;
-      sh = W * (ss & (SPD - 1));
-      if (ww < 0 || ss < slo || ss >= shi) return ~1u;
-      return tbase + 4u * (unsigned)(((ss / SPD - (TC * tq - OV)) * kRows + rr) * kWave + tt);
-    };
-    int shg, shu, shd;
-    const unsigned ag = gaddr(ci, cj, shg), au = gaddr(ci - 1, cj, shu), ad = gaddr(ci - 1, cj - 1, shd);
-    const int wx = ci - 1 - tb * kBandRows, wy = cj - 1 - (TS * tq - YLO);
-    const bool xin = ci >= 1 && wx >= 0, yin = cj >= 1 && wy >= 0 && wy < 256;
-    const unsigned ax = xin ? lds_addr(&xs[cur][0]) + (unsigned)wx : lds_addr(&xs[cur][0]);
-    const unsigned ay = yin ? lds_addr(&ys[cur][0]) + (unsigned)wy : lds_addr(&ys[cur][0]);
-    const unsigned z = tbase;
-    unsigned vx, vy, vg, vu, vd;
-    asm volatile(
-        "ds_read_u8 %0, %5\n\t"
-        "ds_read_u8 %1, %6\n\t"
-        "ds_read_b32 %2, %7\n\t"
-        "ds_read_b32 %3, %8\n\t"
-        "ds_read_b32 %4, %9\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(vx), "=&v"(vy), "=&v"(vg), "=&v"(vu), "=&v"(vd)
-        : "v"(ax), "v"(ay), "v"(ag < ~1u ? ag : z), "v"(au < ~1u ? au : z), "v"(ad < ~1u ? ad : z)
-        : "memory");
-    // rare: cells of the band above / outside the staged window -> global,
-    // in a non-inlined call so the wait for those loads (which also drains
-    // the tile prefetch) stays on this path.
-    if ((!xin && ci >= 1) || (!yin && cj >= 1) || ag == ~1u || au == ~1u || ad == ~1u) {
-      const Five f = tb_fallback<W>(a.mat, pd, bdw, xg, yg, ci, cj, xin, yin, ag == ~1u, au == ~1u, ad == ~1u,
-                                    shg, shu, shd, Five{vx, vy, vg, vu, vd});
-      vx = f.v[0]; vy = f.v[1]; vg = f.v[2]; vu = f.v[3]; vd = f.v[4];
-    }
-    const unsigned g = ag == ~0u ? 0u : (vg >> shg) & MASK;
-    const unsigned gu = au == ~0u ? 0u : (vu >> shu) & MASK;
-    const unsigned gd = ad == ~0u ? 0u : (vd >> shd) & MASK;
-    const bool isD = (vx & 0xffu) == (vy & 0xffu) || ((gd + (unsigned)a.K1 - g) & MASK) == 0u;
-    const bool isU = !isD && ((gu - g) & MASK) == 0u;
-    const unsigned long long mD = __ballot(isD), mU = __ballot(isU);
-    // ---- sequential walk through the block on the two masks (SALU only)
-    int di = 0, dj = 0;
-    while (di < 8 && dj < 8 && i - di > 0 && j - dj > 0) {
-      const int k = di * 8 + dj;
-      const unsigned op = ((mD >> k) & 1ull) ? 'D' : ((mU >> k) & 1ull) ? 'U' : 'L';
-      opw |= op << (8 * (L & 3));
-      if ((L & 3) == 3) {
-        if (lane == 0) *reinterpret_cast<unsigned*>(ops + (L & ~3)) = opw;
-        opw = 0;
-      }
-      ++L;
-      di += op != 'L';
-      dj += op != 'U';
-    }
-    i -= di;
-    j -= dj;
-  }
-  if ((L & 3) != 0 && lane == 0) *reinterpret_cast<unsigned*>(ops + (L & ~3)) = opw;
-  drain();
-  if (lane == 0) {
-    a.oplen[pd.slot] = L;
-    a.endij[pd.slot] = make_int2(i, j);
-  }
-}
 
 // ---------------------------------------------------------------------------
 template <int MODE, int W>
 static hipError_t fill_w(const FillArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((nw_fill<MODE, W>), dim3(grid), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((nw_align<MODE, W>), dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -436,7 +595,7 @@ hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStrea
 template <int MODE, int W>
 static int occ_w() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&nw_fill<MODE, W>), 256, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&nw_align<MODE, W>), 256, 0) != hipSuccess)
     return 1;
   return n > 0 ? n : 1;
 }
@@ -450,19 +609,6 @@ int fill_blocks_per_cu(int mode, int bits) {
     case 16: return p ? occ_w<kProfile, 16>() : occ_w<kCompare, 16>();
     default: return p ? occ_w<kProfile, 32>() : occ_w<kCompare, 32>();
   }
-}
-
-hipError_t launch_traceback(int bits, const TraceArgs& a, hipStream_t s) {
-  const int grid = a.npairs;  // one wave per pair
-  if (grid == 0) return hipSuccess;
-  switch (bits) {
-    case 4: hipLaunchKernelGGL((nw_traceback<4>), dim3(grid), dim3(64), 0, s, a); break;
-    case 8: hipLaunchKernelGGL((nw_traceback<8>), dim3(grid), dim3(64), 0, s, a); break;
-    case 16: hipLaunchKernelGGL((nw_traceback<16>), dim3(grid), dim3(64), 0, s, a); break;
-    case 32: hipLaunchKernelGGL((nw_traceback<32>), dim3(grid), dim3(64), 0, s, a); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
 }
 
 }  // namespace nwk

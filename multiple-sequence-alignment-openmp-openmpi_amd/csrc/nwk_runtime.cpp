@@ -144,7 +144,7 @@ struct nwk_ctx {
   DevBuf d_work;                // matrices | boundary granules | op strings
   bool work_zeroed = false;
   size_t work_zeroed_bytes = 0;
-  DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij;
+  DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij, d_done, d_stamps;
   HostBuf h_pairs, h_tasks, h_oplen, h_endij, h_ops;
 
   nwk_stats stats{};
@@ -173,7 +173,7 @@ void nwk_ctx_destroy(nwk_ctx* c) {
   for (auto& b : c->d_E) b.release();
   c->d_work.release();
   c->d_pairs.release(); c->d_tasks.release(); c->d_ctl.release();
-  c->d_oplen.release(); c->d_endij.release();
+  c->d_oplen.release(); c->d_endij.release(); c->d_done.release(); c->d_stamps.release();
   c->h_pairs.release(); c->h_tasks.release(); c->h_oplen.release();
   c->h_endij.release(); c->h_ops.release();
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
@@ -456,7 +456,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     }
     const int np = (int)(end - pos);
     const int64_t bnd_base_b = round_up(mat * 4, 256);
-    const int64_t ops_base_b = round_up(bnd_base_b + bnd * 8, 256);
+    const int64_t ops_base_b = round_up(bnd_base_b + bnd * 8 + 4096, 256);  // + slack: dummy prefetches
     const int64_t work_b = ops_base_b + ops + 256;
     if ((rc = c->d_work.ensure((size_t)work_b)) != NWK_OK) return rc;
     if (!c->work_zeroed || c->work_zeroed_bytes < c->d_work.cap) {
@@ -491,20 +491,25 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     }
     if ((rc = c->h_tasks.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
     int2* tk = c->h_tasks.as<int2>();
+    // Pair-major (pairs already largest first): a pair's bands are dequeued
+    // together, so pairs finish one after another and each one's traceback
+    // runs concurrently with the fill of the pairs after it.
     int64_t t = 0;
-    for (int b = 0; b < maxb; ++b)
-      for (int q = 0; q < np; ++q)
-        if (b < pd[q].nbands) tk[t++] = make_int2(q, b);
+    for (int q = 0; q < np; ++q)
+      for (int b = 0; b < pd[q].nbands; ++b) tk[t++] = make_int2(q, b);
+    (void)maxb;
     if ((rc = c->d_pairs.ensure(sizeof(PairDesc) * np)) != NWK_OK) return rc;
     if ((rc = c->d_tasks.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
     if ((rc = c->d_oplen.ensure(sizeof(int) * np)) != NWK_OK) return rc;
     if ((rc = c->d_endij.ensure(sizeof(int2) * np)) != NWK_OK) return rc;
+    if ((rc = c->d_done.ensure(sizeof(unsigned) * np)) != NWK_OK) return rc;
     if ((rc = c->h_oplen.ensure(sizeof(int) * np)) != NWK_OK) return rc;
     if ((rc = c->h_endij.ensure(sizeof(int2) * np)) != NWK_OK) return rc;
     if ((rc = c->h_ops.ensure((size_t)ops)) != NWK_OK) return rc;
     HIP_TRY(hipMemcpyAsync(c->d_pairs.p, pd, sizeof(PairDesc) * np, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_tasks.p, tk, sizeof(int2) * ntasks, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(c->d_ctl.p, 0, 256, c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_done.p, 0, sizeof(unsigned) * np, c->stream));
 
     FillArgs fa;
     fa.pairs = c->d_pairs.as<PairDesc>();
@@ -516,36 +521,62 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     fa.bnd = c->d_work.as<unsigned long long>();
     fa.counter = c->d_ctl.as<unsigned>();
     fa.err = c->d_ctl.as<unsigned>() + 16;
+    fa.done = c->d_done.as<unsigned>();
     fa.epoch = ++c->epoch;
     if (fa.epoch == 0) fa.epoch = ++c->epoch;
     fa.K0 = pl.K0;
     fa.K1 = pl.K1;
+    fa.stamps = nullptr;
+    if (c->opts.verbose >= 2) {
+      if ((rc = c->d_stamps.ensure(64 * (size_t)np)) != NWK_OK) return rc;
+      HIP_TRY(hipMemsetAsync(c->d_stamps.p, 0, 64 * (size_t)np, c->stream));
+      fa.stamps = c->d_stamps.as<unsigned long long>();
+    }
+    fa.ops = c->d_work.as<uint8_t>();
+    fa.oplen = c->d_oplen.as<int>();
+    fa.endij = c->d_endij.as<int2>();
+    // One persistent launch: fill bands, and each pair's traceback runs on
+    // the wave that finishes the pair's last band (nw_align).
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(launch_fill(pl.mode, pl.bits, fa, std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-    TraceArgs ta;
-    ta.pairs = fa.pairs;
-    ta.npairs = np;
-    ta.codes = fa.codes;
-    ta.mat = fa.mat;
-    ta.ops = c->d_work.as<uint8_t>();
-    ta.oplen = c->d_oplen.as<int>();
-    ta.endij = c->d_endij.as<int2>();
-    ta.K1 = pl.K1;
-    HIP_TRY(launch_traceback(pl.bits, ta, c->stream));
-    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     unsigned herr = 0;
     HIP_TRY(hipMemcpyAsync(&herr, fa.err, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_oplen.p, ta.oplen, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_endij.p, ta.endij, sizeof(int2) * np, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_oplen.p, fa.oplen, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_endij.p, fa.endij, sizeof(int2) * np, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_ops.p, c->d_work.as<uint8_t>() + ops_base_b, (size_t)ops, hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (herr) return fail(NWK_EKERNEL, "fill kernel: band hand-off timed out (err=%u)", herr);
+    if (herr) {
+      std::vector<unsigned> dn((size_t)np);
+      (void)hipMemcpy(dn.data(), c->d_done.p, sizeof(unsigned) * np, hipMemcpyDeviceToHost);
+      unsigned cnt = 0;
+      (void)hipMemcpy(&cnt, fa.counter, 4, hipMemcpyDeviceToHost);
+      std::vector<int> olv((size_t)np);
+      (void)hipMemcpy(olv.data(), c->d_oplen.p, sizeof(int) * np, hipMemcpyDeviceToHost);
+      std::string d;
+      for (int q = 0; q < np && q < 40; ++q)
+        d += " " + std::to_string(dn[q]) + "/" + std::to_string(pd[q].nbands) + ":" + std::to_string(olv[q]);
+      return fail(NWK_EKERNEL, "kernel hand-off timed out (err=%u); dequeued %u of %lld; done%s",
+                  herr, cnt, (long long)ntasks, d.c_str());
+    }
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
-    st.fill_ms += ms;
-    HIP_TRY(hipEventElapsedTime(&ms, c->ev[1], c->ev[2]));
-    st.traceback_ms += ms;
+    st.fill_ms += ms;  // fill + fused traceback (one launch)
+    if (fa.stamps) {  // per-pair timeline (100 MHz ticks), relative to the earliest fill-done
+      std::vector<unsigned long long> sp(8 * (size_t)np);
+      HIP_TRY(hipMemcpy(sp.data(), fa.stamps, 64 * (size_t)np, hipMemcpyDeviceToHost));
+      unsigned long long t0 = ~0ull;
+      for (int q = 0; q < np; ++q) t0 = std::min(t0, sp[8 * q]);
+      fprintf(stderr, "nwk timeline (ms after first pair filled; kernel %.3f ms): pair m x n: filled -> traced | traceback cycles switch, slow blocks, cycles blocks, blocks, switches, sync loads\n", ms);
+      const int* olh = nullptr;
+      (void)olh;
+      for (int q = 0; q < np; ++q) {
+        const unsigned long long* x = &sp[8 * q];
+        fprintf(stderr, "  %3d %6d x %6d: %8.3f -> %8.3f (trace %.3f) | %.3g %.3g %.3g  blk %llu sw %llu sync %llu\n", q, pd[q].m,
+                pd[q].n, (x[0] - t0) / 1e5, (x[1] - t0) / 1e5, (x[1] - x[0]) / 1e5, (double)x[2], (double)x[3], (double)x[4],
+                x[5], x[6], x[7]);
+      }
+    }
     st.matrix_bytes += mat * 4;
     st.batches += 1;
     st.fill_launches += 1;
