@@ -47,7 +47,8 @@ struct FillArgs {
   uint8_t* ops;            // per pair, reversed traceback moves: 'D','U','L'
   int* oplen;              // per slot
   int2* endij;             // per slot: (i, j) where the traced walk stopped
-  unsigned long long* stamps;  // optional (verbose >= 2): per slot {fill done, traced}, s_memrealtime
+  unsigned long long* stamps;  // optional (verbose >= 2): per-slot diagnostics (see nwk_runtime.cpp)
+  int ntasks_pairs;            // pairs in the batch (diagnostic layout)
   unsigned epoch;
   int K0, K1;              // diag increments in G-space: match, mismatch
 };

@@ -55,6 +55,12 @@ __device__ __forceinline__ void asm_load_E(const unsigned* p, unsigned& e0, unsi
                : "v"(p)
                : "memory");
 }
+__device__ __forceinline__ void asm_load_E2(const unsigned* p, unsigned& e0, unsigned& e1) {
+  asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %2, off offset:256"
+               : "=&v"(e0), "=&v"(e1)
+               : "v"(p)
+               : "memory");
+}
 __device__ __forceinline__ void asm_load_granule(const u64* p, u64& v) {
   asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=&v"(v) : "v"(p) : "memory");
 }
@@ -140,7 +146,10 @@ __device__ __forceinline__ void step_block(int s0, int lane, int (&h)[kRows], in
     const int up0 = __builtin_amdgcn_update_dpp(bv[k], h[kRows - 1], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
     const int dg0 = Up;
     Up = up0;
-    const unsigned ysh = (k < 4 ? e0 : e1) >> (8 * (k & 3));
+    unsigned ysh = (k < 4 ? e0 : e1) >> (8 * (k & 3));
+    // opaque per step: stops the compiler hoisting all 64 lookups of the
+    // block to its top (64 live VGPRs -> 3 instead of 5 waves per SIMD)
+    asm volatile("" : "+v"(ysh));
     int hn[kRows];
 #pragma unroll
     for (int r = 0; r < kRows; ++r)
@@ -161,6 +170,9 @@ __device__ __forceinline__ void step_block(int s0, int lane, int (&h)[kRows], in
       for (int r = 0; r < kRows; ++r)
         __builtin_nontemporal_store(W < 32 ? acc[r] : (unsigned)h[r], mptr + ((k / SPD) * kRows + r) * kWave);
     }
+    // keep each step's substitution lookups inside the step: hoisting all 64
+    // of a block costs ~64 VGPRs and with them 2 waves per SIMD
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -196,7 +208,7 @@ struct TbConf {
   static constexpr int CC = TC + OV;
   static constexpr int TL = 16;                     // lanes (8-row groups) per tile
   static constexpr int TILE = CC * kRows * TL;      // dwords
-  static constexpr int NB = W <= 8 ? 2 : 1;         // double-buffered where LDS allows
+  static constexpr int NB = 1;                       // single buffer: LDS per block bounds fill occupancy
   static constexpr int YLO = 96;                    // y window starts 96 columns below the window
   static_assert(TILE % 64 == 0, "tile = whole DMA instructions");
   static_assert(TS + YLO <= 256, "y window must fit one DMA");
@@ -255,7 +267,7 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
   const uint8_t* yg = a.codes + pd.y_off;
   const unsigned* mb = a.mat + pd.mat_off;
   const bool prof = a.stamps != nullptr;
-  unsigned long long cy_sw = 0, cy_blk = 0, n_blk = 0, n_sw = 0, n_sync = 0, n_slow = 0, tA = 0, tB;
+  unsigned long long cy_sw = 0, cy_blk = 0, n_blk = 0, n_sw = 0, n_sync = 0, tA = 0, tB;
 
   // Stage tile (b, q, t0) into buffer buf by LDS-DMA: lanes [t0, t0+16) of
   // band b, dword columns [TC*q - OV, TC*q + TC) (clamped), the x codes of
@@ -368,7 +380,6 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
           : "memory");
       bg = bu = bd = false;
     } else {  // slow path: band top, border, or outside the window
-      n_slow++;
       const int ci = i - li, cj = j - lj;
       const int slo = C::TS * tq - C::OV * SPD, shi = C::TS * tq + C::TS;
       // LDS address of G(ii, jj), ~0u on the border (G = 0), ~1u if not staged
@@ -434,7 +445,7 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
   }
   if (prof && lane == 0) {
     unsigned long long* st = a.stamps + 8 * pd.slot + 2;
-    st[0] = cy_sw; st[1] = n_slow; st[2] = cy_blk; st[3] = n_blk; st[4] = n_sw; st[5] = n_sync;
+    st[0] = cy_sw; st[1] = cy_blk; st[2] = n_blk; st[3] = (n_sw << 32) | n_sync;
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   flush(Lc);
@@ -449,10 +460,13 @@ template <int MODE, int W>
 __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
   constexpr int SPD = 32 / W;
   __shared__ __attribute__((aligned(16))) int ring_all[4][128];
+  // E window per super-block: E[64sb-64 .. 64sb+64), two slots per wave
+  __shared__ __attribute__((aligned(16))) unsigned ering_all[4][256];
   __shared__ __attribute__((aligned(16))) TbLds<W> tbl[4];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   int* ring = ring_all[wid];
+  unsigned* ering = ering_all[wid];
 
   for (;;) {
     unsigned tk = 0;
@@ -464,7 +478,6 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
     const PairDesc pd = a.pairs[task.x];
     const int band = task.y;
     const int row0 = band * kBandRows + lane * kRows;  // 0-based first row of this lane
-
     unsigned xq[kRows];
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
@@ -489,7 +502,6 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
     const u64* gin = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)(band > 0 ? band - 1 : 0) * bstride + lane;
     const int last_chunk = pd.nchunks > 0 ? pd.nchunks - 1 : 0;
     u64* gout = a.bnd + pd.bnd_off + (int64_t)band * bstride + lane;
-    const unsigned* Ep = a.E + pd.e_off - lane;
     unsigned* mptr = a.mat + pd.mat_off + (int64_t)band * band_dwords(W, pd.sblocks) + lane;
 
     int h[kRows];
@@ -498,11 +510,17 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
     for (int r = 0; r < kRows; ++r) { h[r] = 0; acc[r] = 0; }
     int Up = 0, stage = 0;
     u64 pend = 0;
-    unsigned e0, e1;
-    asm_load_E(Ep, e0, e1);
+    // E window of super-block 0 (columns of steps 0..63 for all lanes):
+    // lane t holds E[-64 + t] and E[t]; later windows are loaded one
+    // super-block ahead and staged in LDS at their super-block's start.
+    const unsigned* Ew = a.E + pd.e_off - 64 + lane;
+    unsigned ew0, ew1;
+    asm_load_E2(Ew, ew0, ew1);
     asm_load_granule(gin, pend);
-    wait_vm_keep<0>(e0, e1, pend);
+    wait_vm_keep<0>(ew0, ew1, pend);
     bool ok = true;
+    u64 cyc_wait = 0, cyc_wait0 = 0, n_wait = 0;
+    const u64 t_task = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
     // stores one block issues after its prefetch loads (<= 63: vmcnt field)
     constexpr int kBlockStores = (8 / SPD) * kRows > 63 ? 63 : (8 / SPD) * kRows;
 
@@ -511,7 +529,14 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
       int bval = 0;
       if (from_above && sb < pd.nchunks) {
         if (!__all((unsigned)(pend >> 32) == a.epoch)) {
+          const u64 tw = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
           pend = wait_granules(gin + 64 * sb, a.epoch, pend, a.err);
+          if (a.stamps) {
+            const u64 d = __builtin_amdgcn_s_memtime() - tw;
+            cyc_wait += d;
+            if (sb == 0) cyc_wait0 += d;
+            ++n_wait;
+          }
           if (!__all((unsigned)(pend >> 32) == a.epoch)) { ok = false; break; }
         }
         bval = (int)(unsigned)pend;
@@ -521,23 +546,27 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
       asm_load_granule(gin + 64 * min(sb + 1, last_chunk), pend);
       int* slot = ring + (sb & 1) * 64;
       slot[lane] = bval;
+      unsigned* ewin = ering + (sb & 1) * 128;
+      ewin[lane] = ew0;
+      ewin[64 + lane] = ew1;
+      // next super-block's E window (covered by the counted wait below)
+      asm_load_E2(Ew + 64 * (sb + 1), ew0, ew1);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
 
       for (int blk = 0; blk < 8; ++blk) {
         const int s0 = sb * 64 + blk * 8;
-        unsigned ne0, ne1;
-        asm_load_E(Ep + s0 + 8, ne0, ne1);  // next block's columns
+        // this lane's columns for steps s0..s0+7: E[s0 - lane], E[s0 - lane + 4]
+        const unsigned e0 = ewin[blk * 8 + 64 - lane], e1 = ewin[blk * 8 + 68 - lane];
         if (sb == 0)
           step_block<MODE, W, true>(s0, lane, h, Up, stage, acc, xq, e0, e1, slot + blk * 8, mptr, a.K0, a.K1);
         else
           step_block<MODE, W, false>(s0, lane, h, Up, stage, acc, xq, e0, e1, slot + blk * 8, mptr, a.K0, a.K1);
         mptr += (8 / SPD) * kRows * kWave;
-        // the prefetch (and the granule issued before it) are older than the
-        // block's kBlockStores stores: waiting for the rest leaves those in flight
-        wait_vm_keep<kBlockStores>(ne0, ne1, pend);
-        e0 = ne0;
-        e1 = ne1;
+        // the window / granule prefetches are older than this block's
+        // kBlockStores stores: waiting for the rest leaves those in flight
+        // (a no-op after block 0)
+        wait_vm_keep<kBlockStores>(ew0, ew1, pend);
       }
       // --- publish chunk sb (columns 64sb-63 .. 64sb of our last row) for band+1
       if (to_below && sb >= 1 && sb <= pd.nchunks) st_granule(gout + 64 * (sb - 1), a.epoch, stage);
@@ -549,6 +578,13 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.stamps && lane == 0) {  // per pair: band cycles, of which waiting on the band above
+      atomicAdd(a.stamps + 8 * pd.slot + 6, (unsigned long long)(__builtin_amdgcn_s_memtime() - t_task));
+      atomicAdd(a.stamps + 8 * pd.slot + 7, (unsigned long long)cyc_wait);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot, (unsigned long long)cyc_wait0);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 1, (unsigned long long)n_wait);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 2, (unsigned long long)pd.sblocks);
+    }
     unsigned prev = 0;
     if (lane == 0) prev = __hip_atomic_fetch_add((gu32*)(a.done + pd.slot), 1u, RLX_AGENT);
     prev = __builtin_amdgcn_readfirstlane(prev);

@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -495,9 +496,24 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     // together, so pairs finish one after another and each one's traceback
     // runs concurrently with the fill of the pairs after it.
     int64_t t = 0;
-    for (int q = 0; q < np; ++q)
-      for (int b = 0; b < pd[q].nbands; ++b) tk[t++] = make_int2(q, b);
-    (void)maxb;
+    static const int order = getenv("NWK_ORDER") ? atoi(getenv("NWK_ORDER")) : 0;
+    if (order == 1) {  // band-major (experiment)
+      for (int b = 0; b < maxb; ++b)
+        for (int q = 0; q < np; ++q)
+          if (b < pd[q].nbands) tk[t++] = make_int2(q, b);
+    } else if (order >= 2) {  // groups of `order` pairs, band-major inside a group (experiment)
+      for (int g0 = 0; g0 < np; g0 += order) {
+        const int g1 = std::min(np, g0 + order);
+        int mb = 0;
+        for (int q = g0; q < g1; ++q) mb = std::max(mb, pd[q].nbands);
+        for (int b = 0; b < mb; ++b)
+          for (int q = g0; q < g1; ++q)
+            if (b < pd[q].nbands) tk[t++] = make_int2(q, b);
+      }
+    } else {
+      for (int q = 0; q < np; ++q)
+        for (int b = 0; b < pd[q].nbands; ++b) tk[t++] = make_int2(q, b);
+    }
     if ((rc = c->d_pairs.ensure(sizeof(PairDesc) * np)) != NWK_OK) return rc;
     if ((rc = c->d_tasks.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
     if ((rc = c->d_oplen.ensure(sizeof(int) * np)) != NWK_OK) return rc;
@@ -527,9 +543,10 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     fa.K0 = pl.K0;
     fa.K1 = pl.K1;
     fa.stamps = nullptr;
+    fa.ntasks_pairs = np;
     if (c->opts.verbose >= 2) {
-      if ((rc = c->d_stamps.ensure(64 * (size_t)np)) != NWK_OK) return rc;
-      HIP_TRY(hipMemsetAsync(c->d_stamps.p, 0, 64 * (size_t)np, c->stream));
+      if ((rc = c->d_stamps.ensure(88 * (size_t)np)) != NWK_OK) return rc;
+      HIP_TRY(hipMemsetAsync(c->d_stamps.p, 0, 88 * (size_t)np, c->stream));
       fa.stamps = c->d_stamps.as<unsigned long long>();
     }
     fa.ops = c->d_work.as<uint8_t>();
@@ -563,19 +580,30 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     st.fill_ms += ms;  // fill + fused traceback (one launch)
     if (fa.stamps) {  // per-pair timeline (100 MHz ticks), relative to the earliest fill-done
-      std::vector<unsigned long long> sp(8 * (size_t)np);
-      HIP_TRY(hipMemcpy(sp.data(), fa.stamps, 64 * (size_t)np, hipMemcpyDeviceToHost));
+      std::vector<unsigned long long> sp(11 * (size_t)np);
+      HIP_TRY(hipMemcpy(sp.data(), fa.stamps, 88 * (size_t)np, hipMemcpyDeviceToHost));
       unsigned long long t0 = ~0ull;
       for (int q = 0; q < np; ++q) t0 = std::min(t0, sp[8 * q]);
-      fprintf(stderr, "nwk timeline (ms after first pair filled; kernel %.3f ms): pair m x n: filled -> traced | traceback cycles switch, slow blocks, cycles blocks, blocks, switches, sync loads\n", ms);
-      const int* olh = nullptr;
-      (void)olh;
+      fprintf(stderr, "nwk timeline (ms after first pair filled; kernel %.3f ms): pair m x n: filled -> traced | "
+                      "trace cycles switch/blocks, blocks, switches/sync | fill band-cycles, %% waiting on band above\n", ms);
+      double bc = 0, wc = 0;
       for (int q = 0; q < np; ++q) {
         const unsigned long long* x = &sp[8 * q];
-        fprintf(stderr, "  %3d %6d x %6d: %8.3f -> %8.3f (trace %.3f) | %.3g %.3g %.3g  blk %llu sw %llu sync %llu\n", q, pd[q].m,
-                pd[q].n, (x[0] - t0) / 1e5, (x[1] - t0) / 1e5, (x[1] - x[0]) / 1e5, (double)x[2], (double)x[3], (double)x[4],
-                x[5], x[6], x[7]);
+        bc += (double)x[6];
+        wc += (double)x[7];
+        fprintf(stderr, "  %3d %6d x %6d: %8.3f -> %8.3f (trace %.3f) | %.3g %.3g %llu %llu/%llu | %.3g %.1f%%\n", q,
+                pd[q].m, pd[q].n, (x[0] - t0) / 1e5, (x[1] - t0) / 1e5, (x[1] - x[0]) / 1e5, (double)x[2], (double)x[3],
+                x[4], x[5] >> 32, x[5] & 0xffffffffull, (double)x[6], x[6] ? 100.0 * (double)x[7] / (double)x[6] : 0.0);
       }
+      double w0 = 0, nw = 0, nsb = 0;
+      for (int q = 0; q < np; ++q) {
+        w0 += (double)sp[8 * (size_t)np + 3 * q];
+        nw += (double)sp[8 * (size_t)np + 3 * q + 1];
+        nsb += (double)sp[8 * (size_t)np + 3 * q + 2];
+      }
+      fprintf(stderr, "  all bands: %.4g cycles, %.1f%% waiting on the band above (%.1f%% before the first chunk); "
+                      "%.4g waits over %.4g super-blocks\n",
+              bc, bc > 0 ? 100.0 * wc / bc : 0.0, bc > 0 ? 100.0 * w0 / bc : 0.0, nw, nsb);
     }
     st.matrix_bytes += mat * 4;
     st.batches += 1;
