@@ -9,6 +9,11 @@ constexpr int kWave = 64;
 constexpr int kRows = 8;                  // DP rows per lane (R)
 constexpr int kBandRows = kWave * kRows;  // rows per band = one wave's task
 constexpr int kEPad = 64;                 // E entries before column 0
+// Sequence-code buffer padding.  The traceback stages 256-byte windows by
+// LDS-DMA: y windows start up to 96 bytes before a sequence, x windows end up
+// to ~660 bytes past the last 512-row band's first row.
+constexpr int kCodesFrontPad = 128;
+constexpr int kCodesTailPad = 1024;
 
 // Recurrence variants (see DESIGN.md "Kernels").
 enum Mode : int {

@@ -212,6 +212,7 @@ struct TbConf {
   static constexpr int YLO = 96;                    // y window starts 96 columns below the window
   static_assert(TILE % 64 == 0, "tile = whole DMA instructions");
   static_assert(TS + YLO <= 256, "y window must fit one DMA");
+  static_assert(YLO <= kCodesFrontPad, "y windows must stay inside the codes buffer");
 };
 
 template <int W>

@@ -143,8 +143,7 @@ struct nwk_ctx {
 
   // batch buffers
   DevBuf d_work;                // matrices | boundary granules | op strings
-  bool work_zeroed = false;
-  size_t work_zeroed_bytes = 0;
+  int64_t clean_b = 0;          // leading bytes of d_work holding only zeros / old-epoch granules
   DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij, d_done, d_stamps;
   HostBuf h_pairs, h_tasks, h_oplen, h_endij, h_ops;
 
@@ -239,7 +238,7 @@ int nwk_set_sequences(nwk_ctx* c, const uint8_t* seqs, const int64_t* offsets, i
   // layout: codes 8-aligned; E with kEPad entries before column 0 and 256 after the end
   c->c_off.resize(k);
   c->e_off.resize(k);
-  int64_t co = 64, eo = 0;  // codes: 64-byte front pad (traceback y windows start 64 before)
+  int64_t co = kCodesFrontPad, eo = 0;
   for (int s = 0; s < k; ++s) {
     const int64_t L = c->off[s + 1] - c->off[s];
     c->c_off[s] = co;
@@ -260,8 +259,8 @@ namespace {
 int build_encoding(nwk_ctx* c, int kind) {
   if (c->built[kind]) return NWK_OK;
   const int k = c->k;
-  // + 512-byte tail pad: the traceback stages whole 512-row x windows and 256-byte y windows
-  const int64_t ncodes = (k ? c->c_off[k - 1] + round_up(c->off[k] - c->off[k - 1] + 8, 8) : 64) + 512;
+  const int64_t ncodes =
+      (k ? c->c_off[k - 1] + round_up(c->off[k] - c->off[k - 1] + 8, 8) : kCodesFrontPad) + kCodesTailPad;
   const int64_t nE = k ? c->e_off[k - 1] - kEPad + kEPad + (c->off[k] - c->off[k - 1]) + 256 : 64;
   std::vector<uint8_t> codes((size_t)ncodes, 0);
   std::vector<uint32_t> E((size_t)nE, 0);
@@ -456,16 +455,22 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
       ++end;
     }
     const int np = (int)(end - pos);
-    const int64_t bnd_base_b = round_up(mat * 4, 256);
-    const int64_t ops_base_b = round_up(bnd_base_b + bnd * 8 + 4096, 256);  // + slack: dummy prefetches
-    const int64_t work_b = ops_base_b + ops + 256;
+    // Layout: [granules | slack | matrices | op strings].  The granule region
+    // always starts at offset 0, so across batches it only ever overlaps
+    // older granules or zeros -- never stale matrix words, whose upper halves
+    // could equal a future epoch tag.  Bytes past the previous batch's
+    // granule region are zeroed before they are used as granules.
+    const int64_t bnd_need_b = bnd * 8 + 4096;  // + slack: band 0's dummy prefetches
+    const int64_t mat_base_b = round_up(bnd_need_b, 256);
+    const int64_t ops_base_b = round_up(mat_base_b + mat * 4, 256);
+    const int64_t work_b = ops_base_b + ops + 256;  // + slack: traceback tile overrun of the last band
+    void* const old_work = c->d_work.p;
     if ((rc = c->d_work.ensure((size_t)work_b)) != NWK_OK) return rc;
-    if (!c->work_zeroed || c->work_zeroed_bytes < c->d_work.cap) {
-      // granule tags must never hold a future epoch: zero once per allocation
-      HIP_TRY(hipMemsetAsync(c->d_work.p, 0, c->d_work.cap, c->stream));
-      c->work_zeroed = true;
-      c->work_zeroed_bytes = c->d_work.cap;
+    if (c->d_work.p != old_work) c->clean_b = 0;
+    if (bnd_need_b > c->clean_b) {
+      HIP_TRY(hipMemsetAsync(c->d_work.as<uint8_t>() + c->clean_b, 0, (size_t)(bnd_need_b - c->clean_b), c->stream));
     }
+    c->clean_b = bnd_need_b;
     // ---- descriptors and dependency-ordered band tasks (band-major)
     if ((rc = c->h_pairs.ensure(sizeof(PairDesc) * np)) != NWK_OK) return rc;
     PairDesc* pd = c->h_pairs.as<PairDesc>();
@@ -477,8 +482,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
       d.x_off = c->c_off[w.i];
       d.y_off = c->c_off[w.j];
       d.e_off = c->e_off[w.j];
-      d.mat_off = mo;
-      d.bnd_off = bnd_base_b / 8 + bo;
+      d.mat_off = mat_base_b / 4 + mo;
+      d.bnd_off = bo;
       d.ops_off = ops_base_b + oo;
       d.m = w.m;
       d.n = w.n;
@@ -554,6 +559,12 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     fa.endij = c->d_endij.as<int2>();
     // One persistent launch: fill bands, and each pair's traceback runs on
     // the wave that finishes the pair's last band (nw_align).
+    if (c->opts.verbose >= 3) {
+      fprintf(stderr, "nwk batch %d: pairs [%zu, %zu) ids %lld..%lld, %lld tasks, work %.3f GB (mat %.3f, bnd %.3f, ops %.3f)\n",
+              st.batches, pos, end, (long long)dp[pos].id, (long long)dp[end - 1].id, (long long)ntasks, work_b / 1e9,
+              mat * 4 / 1e9, bnd * 8 / 1e9, ops / 1e9);
+      fflush(stderr);
+    }
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(launch_fill(pl.mode, pl.bits, fa, std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
