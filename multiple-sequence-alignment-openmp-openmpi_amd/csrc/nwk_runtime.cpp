@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <string>
 #include <thread>
@@ -145,7 +146,8 @@ struct nwk_ctx {
   DevBuf d_work;                // matrices | boundary granules | op strings
   int64_t clean_b = 0;          // leading bytes of d_work holding only zeros / old-epoch granules
   DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij, d_done, d_stamps;
-  HostBuf h_pairs, h_tasks, h_oplen, h_endij, h_ops;
+  HostBuf h_tasks;
+  HostBuf h_pairs[2], h_oplen[2], h_endij[2], h_ops[2];  // double-buffered: batch b+1 runs while b finalizes
 
   nwk_stats stats{};
 };
@@ -174,8 +176,10 @@ void nwk_ctx_destroy(nwk_ctx* c) {
   c->d_work.release();
   c->d_pairs.release(); c->d_tasks.release(); c->d_ctl.release();
   c->d_oplen.release(); c->d_endij.release(); c->d_done.release(); c->d_stamps.release();
-  c->h_pairs.release(); c->h_tasks.release(); c->h_oplen.release();
-  c->h_endij.release(); c->h_ops.release();
+  c->h_tasks.release();
+  for (int b = 0; b < 2; ++b) {
+    c->h_pairs[b].release(); c->h_oplen[b].release(); c->h_endij[b].release(); c->h_ops[b].release();
+  }
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -439,6 +443,13 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
   const int grid = bpc * c->cus;
   float ms = 0;
 
+  // at most one finalize in flight; joined on every exit path
+  struct Joiner {
+    std::thread t;
+    void start(std::function<void()> f) { t = std::thread(std::move(f)); }
+    void join() { if (t.joinable()) t.join(); }
+    ~Joiner() { join(); }
+  } fin;
   size_t pos = 0;
   while (pos < dp.size()) {
     // ---- form a batch that fits the HBM budget
@@ -472,8 +483,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     }
     c->clean_b = bnd_need_b;
     // ---- descriptors and dependency-ordered band tasks (band-major)
-    if ((rc = c->h_pairs.ensure(sizeof(PairDesc) * np)) != NWK_OK) return rc;
-    PairDesc* pd = c->h_pairs.as<PairDesc>();
+    const int par = st.batches & 1;  // host buffer set of this batch
+    if ((rc = c->h_pairs[par].ensure(sizeof(PairDesc) * np)) != NWK_OK) return rc;
+    PairDesc* pd = c->h_pairs[par].as<PairDesc>();
     int64_t mo = 0, bo = 0, oo = 0, ntasks = 0;
     int maxb = 0;
     for (int q = 0; q < np; ++q) {
@@ -524,9 +536,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     if ((rc = c->d_oplen.ensure(sizeof(int) * np)) != NWK_OK) return rc;
     if ((rc = c->d_endij.ensure(sizeof(int2) * np)) != NWK_OK) return rc;
     if ((rc = c->d_done.ensure(sizeof(unsigned) * np)) != NWK_OK) return rc;
-    if ((rc = c->h_oplen.ensure(sizeof(int) * np)) != NWK_OK) return rc;
-    if ((rc = c->h_endij.ensure(sizeof(int2) * np)) != NWK_OK) return rc;
-    if ((rc = c->h_ops.ensure((size_t)ops)) != NWK_OK) return rc;
+    if ((rc = c->h_oplen[par].ensure(sizeof(int) * np)) != NWK_OK) return rc;
+    if ((rc = c->h_endij[par].ensure(sizeof(int2) * np)) != NWK_OK) return rc;
+    if ((rc = c->h_ops[par].ensure((size_t)ops)) != NWK_OK) return rc;
     HIP_TRY(hipMemcpyAsync(c->d_pairs.p, pd, sizeof(PairDesc) * np, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_tasks.p, tk, sizeof(int2) * ntasks, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(c->d_ctl.p, 0, 256, c->stream));
@@ -570,9 +582,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     unsigned herr = 0;
     HIP_TRY(hipMemcpyAsync(&herr, fa.err, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_oplen.p, fa.oplen, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_endij.p, fa.endij, sizeof(int2) * np, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_ops.p, c->d_work.as<uint8_t>() + ops_base_b, (size_t)ops, hipMemcpyDeviceToHost,
+    HIP_TRY(hipMemcpyAsync(c->h_oplen[par].p, fa.oplen, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_endij[par].p, fa.endij, sizeof(int2) * np, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_ops[par].p, c->d_work.as<uint8_t>() + ops_base_b, (size_t)ops, hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (herr) {
@@ -619,21 +631,30 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     st.matrix_bytes += mat * 4;
     st.batches += 1;
     st.fill_launches += 1;
-    // ---- host finalize
-    const int* ol = c->h_oplen.as<int>();
-    const int2* ej = c->h_endij.as<int2>();
-    const uint8_t* hops = c->h_ops.as<uint8_t>();
-    parallel_for(a1 ? 1 : c->host_threads, np, [&](int64_t q) {
-      const PairWork& w = dp[pos + q];
-      const PairDesc& d = pd[q];
-      Finalized f;
-      finalize_pair(c->seqs.data() + c->off[w.i], w.m, c->seqs.data() + c->off[w.j], w.n, pxy, pgap,
-                    hops + (d.ops_off - ops_base_b), ol[q], ej[q].x, ej[q].y, &f, a1, a2);
-      penalties[w.out] = f.penalty;
-      memcpy(hashes + 64 * w.out, f.hash, 64);
-    });
+    // ---- host finalize, overlapped with the next batch's kernel: it runs on
+    // its own thread over this batch's host buffer set while the loop goes
+    // on to set up, launch and wait for batch b+1 (buffer set par ^ 1).
+    fin.join();
+    const int* ol = c->h_oplen[par].as<int>();
+    const int2* ej = c->h_endij[par].as<int2>();
+    const uint8_t* hops = c->h_ops[par].as<uint8_t>();
+    const PairWork* dw = dp.data() + pos;
+    auto job = [c, a1, a2, np, dw, pd, ol, ej, hops, ops_base_b, pxy, pgap, penalties, hashes]() {
+      parallel_for(a1 ? 1 : c->host_threads, np, [&](int64_t q) {
+        const PairWork& w = dw[q];
+        const PairDesc& d = pd[q];
+        Finalized f;
+        finalize_pair(c->seqs.data() + c->off[w.i], w.m, c->seqs.data() + c->off[w.j], w.n, pxy, pgap,
+                      hops + (d.ops_off - ops_base_b), ol[q], ej[q].x, ej[q].y, &f, a1, a2);
+        penalties[w.out] = f.penalty;
+        memcpy(hashes + 64 * w.out, f.hash, 64);
+      });
+    };
+    if (end < dp.size()) fin.start(job);
+    else job();
     pos = end;
   }
+  fin.join();
   st.total_ms = now_ms() - t_start;
   c->stats = st;
   if (c->opts.verbose)
