@@ -3,7 +3,8 @@ usage: python tools/timeit.py [lib_dir ...]  (each lib dir holds a libnwk.so var
 import sys, os, time, ctypes, importlib
 sys.path.insert(0, "multiple-sequence-alignment-openmp-openmpi_amd")
 import numpy as np
-import seqalign
+import seqalign, json
+GOLD = {c["name"]: c for c in json.load(open("tests/golden/golden.json"))["cases"]}["big13"]["hash"]
 wl = os.environ.get("WL", "big13")
 reps = int(os.environ.get("REPS", "5"))
 t = open("tests/golden/data/mseq-big13-example.txt", "rb").read()
@@ -12,12 +13,13 @@ libs = sys.argv[1:] or [os.path.dirname(seqalign.LIB_PATH)]
 for d in libs * int(os.environ.get("ROUNDS", "1")):
     seqalign._lib = None
     seqalign.load_library(os.path.join(d, "libnwk.so"))
-    e = seqalign.Engine(device=0)
+    e = seqalign.Engine(device=0, verbose=int(os.environ.get("V", "0")))
     e.set_sequences(g)
     ids = np.arange(78, dtype=np.int64)
     ks, ws = [], []
     for r in range(reps):
-        t0 = time.perf_counter(); e.align_pairs(ids, pxy, pgap); ws.append(time.perf_counter() - t0)
+        t0 = time.perf_counter(); pen, hs = e.align_pairs(ids, pxy, pgap); ws.append(time.perf_counter() - t0)
+        assert seqalign.chain_hash(hs) == GOLD, "big13 hash mismatch"
         ks.append(e.stats()["fill_ms"])
     e.close()
-    print("%-40s kernel ms min %.2f med %.2f | wall ms min %.2f med %.2f" % (d, min(ks), sorted(ks)[len(ks)//2], 1e3*min(ws), 1e3*sorted(ws)[len(ws)//2]), flush=True)
+    print("timeit %-40s kernel ms min %.2f med %.2f | wall ms min %.2f med %.2f" % (d, min(ks), sorted(ks)[len(ks)//2], 1e3*min(ws), 1e3*sorted(ws)[len(ws)//2]), flush=True)
