@@ -68,7 +68,7 @@ typedef struct nwk_stats {
   int64_t matrix_bytes;      /* HBM bytes of the stored DP matrices */
   int32_t batches;           /* workspace batches used */
   int32_t bits;              /* storage width used */
-  int32_t mode;              /* 0 = profile, 1 = compare, 2 = literal */
+  int32_t mode;              /* 0 = profile, 1 = compare, 2 = literal, 3 = affine */
   int32_t fill_launches;     /* fill-kernel launches in the call */
   int32_t reserved[4];
 } nwk_stats;
@@ -124,6 +124,26 @@ int nwk_get_minimum_penalties(const uint8_t *seqs, const int64_t *offsets, int32
 int nwk_get_minimum_penalty(nwk_ctx *ctx, const uint8_t *x, int32_t m, const uint8_t *y,
                             int32_t n, int32_t pxy, int32_t pgap, uint8_t *a1, uint8_t *a2,
                             int32_t *alen, int32_t *penalty);
+
+/*
+ * Affine-gap variant (SURVEY.md §8 a9 -- no reference counterpart; the build
+ * defines it, see oracle/nw_oracle.c nwo_pair_affine):
+ *   E = min(E[i][j-1] + ge, H[i][j-1] + go + ge), F = min(F[i-1][j] + ge, H[i-1][j] + go + ge),
+ *   H = x_i == y_j ? H[i-1][j-1] : min(H[i-1][j-1] + pxy, F, E),
+ *   H[i][0] = go + i*ge, H[0][j] = go + j*ge, H[0][0] = 0.
+ * Traceback DIAG > UP > LEFT as the reference, a gap closing (returning to
+ * H) whenever its open term ties; prefix, trim and hashes as the linear path.
+ * With go = 0, ge = pgap every result equals the linear entry point's.
+ * Requires pxy, go, ge >= 0 (NWK_EINVAL otherwise).
+ */
+int nwk_align_pairs_affine(nwk_ctx *ctx, const int64_t *pair_ids, int64_t npairs, int32_t pxy,
+                           int32_t go, int32_t ge, int32_t *penalties, uint8_t *problem_hash);
+int nwk_get_minimum_penalty_affine(nwk_ctx *ctx, const uint8_t *x, int32_t m, const uint8_t *y,
+                                   int32_t n, int32_t pxy, int32_t go, int32_t ge, uint8_t *a1,
+                                   uint8_t *a2, int32_t *alen, int32_t *penalty);
+int nwk_get_minimum_penalties_affine(const uint8_t *seqs, const int64_t *offsets, int32_t k,
+                                     int32_t pxy, int32_t go, int32_t ge, int32_t *penalties,
+                                     char *hash_hex, const nwk_opts *opts);
 
 /*
  * Deterministic cell-cost shard of the P pairs of a sequence set over world

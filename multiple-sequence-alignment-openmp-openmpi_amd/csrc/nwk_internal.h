@@ -20,6 +20,7 @@ enum Mode : int {
   kProfile = 0,  // |alphabet| <= 4, penalties >= 0: signed-byte substitution profile
   kCompare = 1,  // any bytes, penalties >= 0: byte compare + select
   kLiteral = 2,  // any penalties: skel:215-224 literally (match ? diag : min3)
+  kAffine = 3,   // affine gaps: 4-bit traceback codes, compare mode
 };
 
 // One pair of the batch.  All offsets are element offsets into the
@@ -55,7 +56,10 @@ struct FillArgs {
   unsigned long long* stamps;  // optional (verbose >= 2): per-slot diagnostics (see nwk_runtime.cpp)
   int ntasks_pairs;            // pairs in the batch (diagnostic layout)
   unsigned epoch;
-  int K0, K1;              // diag increments in G-space: match, mismatch
+  int K0, K1;              // diag increments in G-space: match, mismatch (kAffine: K1 = pxy)
+  int go, ge;              // kAffine: gap open / extend
+  int dbg_notrace;         // debug: skip the affine traceback
+  unsigned* prog;          // debug: per-wave progress markers (NWK_WATCHDOG)
 };
 
 // Launchers (nwk_kernels.hip).  bits in {4, 8, 16, 32}.

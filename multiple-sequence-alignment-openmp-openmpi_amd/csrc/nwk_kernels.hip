@@ -602,6 +602,345 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
 }
 
 
+// ===========================================================================
+// Affine-gap variant (build-defined, see oracle
+// nwo_pair_affine):
+//   E = min(E[i][j-1] + ge, H[i][j-1] + go + ge)      F = min(F[i-1][j] + ge, H[i-1][j] + go + ge)
+//   H = x == y ? H[i-1][j-1] : min(H[i-1][j-1] + pxy, F, E)
+// in plain H-space int32 (no relabelling: three matrices' worth of state).
+// Same band / skew / hand-off machinery as nw_align, with two boundary rows
+// per band (H and F of its last row) and, per cell, a 4-bit traceback code
+// instead of G mod 16:
+//   bits 1:0  H's source: 0 diagonal (match, or H[i-1][j-1] + pxy == H),
+//             1 F (F == H), 2 E        -- the reference's DIAG > UP > LEFT order
+//   bit 2     F opened here (H[i-1][j] + go + ge <= F[i-1][j] + ge: open wins ties)
+//   bit 3     E opened here
+// The traceback walks these codes with a three-state machine.
+// ===========================================================================
+constexpr int kAffInf = 0x3fffffff;
+
+template <bool MASK>
+__device__ __forceinline__ void step_block_affine(int s0, int lane, int (&h)[kRows], int (&e)[kRows], int& Up,
+                                                  int& f7, int& stH, int& stF, unsigned (&acc)[kRows],
+                                                  const unsigned (&xq)[kRows], unsigned e0, unsigned e1,
+                                                  const int* bH, const int* bF, unsigned* mptr, int pxy, int goe,
+                                                  int ge) {
+  const int4 hA = *reinterpret_cast<const int4*>(bH), hB = *reinterpret_cast<const int4*>(bH + 4);
+  const int4 fA = *reinterpret_cast<const int4*>(bF), fB = *reinterpret_cast<const int4*>(bF + 4);
+  const int bh[8] = {hA.x, hA.y, hA.z, hA.w, hB.x, hB.y, hB.z, hB.w};
+  const int bf[8] = {fA.x, fA.y, fA.z, fA.w, fB.x, fB.y, fB.z, fB.w};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    stH = __builtin_amdgcn_update_dpp(h[kRows - 1], stH, 0x130 /*wave_shl:1*/, 0xf, 0xf, false);
+    stF = __builtin_amdgcn_update_dpp(f7, stF, 0x130, 0xf, 0xf, false);
+    const int uh = __builtin_amdgcn_update_dpp(bh[k], h[kRows - 1], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
+    const int uf = __builtin_amdgcn_update_dpp(bf[k], f7, 0x138, 0xf, 0xf, false);
+    const int dg0 = Up;
+    Up = uh;
+    unsigned ysh = (k < 4 ? e0 : e1) >> (8 * (k & 3));
+    asm volatile("" : "+v"(ysh));
+    const unsigned yb = ysh & 0xffu;
+    int hn[kRows], en[kRows], fprev = uf, hprev = uh;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      const int hd = r ? h[r - 1] : dg0;
+      const int eo = h[r] + goe, ee = e[r] + ge;
+      const int ev = min(eo, ee);
+      const int fo = hprev + goe, fe = fprev + ge;
+      const int fv = min(fo, fe);
+      const bool match = yb == xq[r];
+      const int hc = hd + (match ? 0 : pxy);
+      const int hv = match ? hd : min(min(hc, fv), ev);
+      const unsigned src = hc == hv ? 0u : (fv == hv ? 1u : 2u);
+      const unsigned code = src | (fo <= fe ? 4u : 0u) | (eo <= ee ? 8u : 0u);
+      acc[r] = __builtin_amdgcn_alignbit(code, acc[r], 4);
+      hn[r] = hv;
+      en[r] = ev;
+      hprev = hv;
+      fprev = fv;
+    }
+    if constexpr (MASK) {  // columns j <= 0 keep the border (H = go + i ge, E = +inf)
+      const bool valid = (s0 + k) >= lane;
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) {
+        hn[r] = valid ? hn[r] : h[r];
+        en[r] = valid ? en[r] : e[r];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) { h[r] = hn[r]; e[r] = en[r]; }
+    f7 = fprev;
+    if (k == 7) {
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) __builtin_nontemporal_store(acc[r], mptr + r * kWave);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm_keep4(unsigned& a, unsigned& b, u64& c, u64& d) {
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N) : "memory");
+}
+
+// Traceback of one affine pair on its 4-bit codes (same LDS tile staging as
+// trace_pair).  Per 8x8 block every lane loads its cell's code; the walk is
+// a scalar three-state machine over v_readlane.  Moves are emitted reversed:
+// 'D', 'U'/'L' (gap extended) and 'u'/'l' (the gap's first column: the host
+// charges go + ge there, ge for the others).
+__device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairDesc& pd, TbLds<4>& L, int lane, unsigned* prog) {
+  using C = TbConf<4>;
+  constexpr int SPD = C::SPD;
+  const int64_t bdw = band_dwords(4, pd.sblocks);
+  const int ncols = 64 * pd.sblocks / SPD;
+  const unsigned* mb = a.mat + pd.mat_off;
+  const int lane_off = (lane >> 4) * kWave + (lane & 15);
+  auto issue = [&](int b, int q, int t0) {
+    const unsigned* src = mb + (int64_t)b * bdw + t0 + lane_off;
+#pragma unroll
+    for (int k = 0; k < C::TILE / 64; ++k) {
+      int c = C::TC * q - C::OV + (k >> 1);
+      c = c < 0 ? 0 : (c >= ncols ? ncols - 1 : c);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (int64_t)c * (kRows * kWave) + (k & 1) * 4 * kWave),
+                                       (lds_void*)&L.tile[0][64 * k], 4, 0, 0);
+    }
+  };
+  auto drain = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+  uint8_t* ops = a.ops + pd.ops_off;
+  int i = pd.m, j = pd.n, Lc = 0, flushed = 0, tb = -1, tq = 0, tt0 = 0;
+  unsigned st = 0;  // 0 = H, 1 = F, 2 = E
+  bool bad = false;
+  const unsigned ob = lds_addr(&L.obuf[0]);
+  auto flush = [&](int upto) {
+    const int from = flushed & ~3;
+    for (int o = from + 4 * lane; o < upto; o += 256) {
+      unsigned v;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ob + (unsigned)(o & 255)) : "memory");
+      *reinterpret_cast<unsigned*>(ops + o) = v;
+    }
+    flushed = upto;
+  };
+  const int li = lane >> 3, lj = lane & 7;
+  unsigned nit = 0;
+  while (i > 0 && j > 0) {
+    ++nit;
+    if (prog && lane == 0) __hip_atomic_store((gu32*)prog, 0x50000000u | ((nit & 0xff) << 20) | ((unsigned)(i & 0x3ff) << 10) | (unsigned)(j & 0x3ff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const int w = (i - 1) & (kBandRows - 1);
+    const int t = w >> 3;
+    const int b = (i - 1) / kBandRows;
+    {
+      const int tl = t > 0 ? t - 1 : 0;
+      const int s = j - 1 + t;
+      if (b != tb || s < C::TS * tq || tl < tt0 || t >= tt0 + C::TL) {
+        const int q = s / C::TS;
+        drain();
+        flush(Lc & ~3);
+        const int nt0 = max(0, t - (C::TL - 3));
+        issue(b, q, nt0);
+        drain();
+        tb = b; tq = q; tt0 = nt0;
+      }
+    }
+    // this lane's cell (ci, cj) = (i - li, j - lj)
+    const int ci = i - li, cj = j - lj;
+    unsigned code = 0;
+    if (ci >= 1 && cj >= 1) {
+      const int ww = ci - 1 - tb * kBandRows;
+      const int tt = ww >> 3, rr = ww & 7, ss = cj - 1 + tt;
+      const int slo = C::TS * tq - C::OV * SPD, shi = C::TS * tq + C::TS;
+      const int cbase = C::TC * tq - C::OV;
+      unsigned v;
+      if (ww >= 0 && tt >= tt0 && tt < tt0 + C::TL && ss >= slo && ss < shi) {
+        const unsigned ad = lds_addr(&L.tile[0][0]) + 4u * (unsigned)(((ss / SPD - cbase) * kRows + rr) * C::TL + (tt - tt0));
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ad) : "memory");
+        code = (v >> (4 * (ss & (SPD - 1)))) & 15u;
+      } else {
+        code = getG_global<4>(a.mat, pd, bdw, ci, cj);
+      }
+    }
+    if (prog && lane == 0) __hip_atomic_store((gu32*)prog, 0x51000000u | (code & 0xff) << 8 | (nit & 0xff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // scalar walk through the block
+    int di = 0, dj = 0;
+    for (;;) {
+      const unsigned c = __builtin_amdgcn_readlane(code, di * 8 + dj);
+      unsigned op;
+      op = 0;
+      if (st == 0) {
+        const unsigned src = c & 3u;
+        if (src == 0) {
+          op = 'D';
+          ++di; ++dj;
+        } else if (src < 3) {
+          st = src;  // 1 = F, 2 = E: the gap step below runs from this same cell
+        } else {
+          bad = true;  // not a code the fill writes
+          break;
+        }
+      }
+      if (st == 1) {
+        const bool open = (c >> 2) & 1u;
+        op = open ? 'u' : 'U';
+        st = open ? 0u : 1u;
+        ++di;
+      } else if (st == 2) {
+        const bool open = (c >> 3) & 1u;
+        op = open ? 'l' : 'L';
+        st = open ? 0u : 2u;
+        ++dj;
+      }
+      asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(op) : "memory");
+      ++Lc;
+      if (di > 7 || dj > 7 || i - di <= 0 || j - dj <= 0) break;
+    }
+    i -= di;
+    j -= dj;
+    if (prog && lane == 0) __hip_atomic_store((gu32*)prog, 0x52000000u | ((unsigned)di << 12) | ((unsigned)dj << 8) | (nit & 0xff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (Lc - flushed >= 160) flush(Lc & ~3);
+    if (bad || Lc > pd.m + pd.n) {
+      if (lane == 0) atomicOr(a.err, 16u);
+      break;
+    }
+  }
+  if (prog && lane == 0) __hip_atomic_store((gu32*)prog, 0x53000000u | (nit & 0xffff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  flush(Lc);
+  if (prog && lane == 0) __hip_atomic_store((gu32*)prog, 0x54000000u | (nit & 0xffff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  drain();
+  if (prog && lane == 0) __hip_atomic_store((gu32*)prog, 0x55000000u | (nit & 0xffff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane == 0) {
+    a.oplen[pd.slot] = Lc;
+    a.endij[pd.slot] = make_int2(i, j);
+  }
+}
+
+__global__ __launch_bounds__(256) void nw_align_affine(FillArgs a) {
+  constexpr int W = 4, SPD = 8;
+  __shared__ __attribute__((aligned(16))) int ringH_all[4][128];
+  __shared__ __attribute__((aligned(16))) int ringF_all[4][128];
+  __shared__ __attribute__((aligned(16))) unsigned ering_all[4][256];
+  __shared__ __attribute__((aligned(16))) TbLds<W> tbl[4];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  int* ringH = ringH_all[wid];
+  int* ringF = ringF_all[wid];
+  unsigned* ering = ering_all[wid];
+  const int pxy = a.K1, go = a.go, ge = a.ge, goe = a.go + a.ge;
+  unsigned* prog = a.prog ? a.prog + blockIdx.x * 4 + wid : nullptr;
+#define PROG(v) do { if (prog && lane == 0) __hip_atomic_store((gu32*)prog, (unsigned)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); } while (0)
+
+  for (;;) {
+    unsigned tk = 0;
+    if (lane == 0) tk = atomicAdd(a.counter, 1u);
+    tk = __builtin_amdgcn_readfirstlane(tk);
+    PROG(0x10000000u | tk);
+    if (tk >= (unsigned)a.ntasks) { PROG(0x60000000u); return; }
+    if (__hip_atomic_load((gu32*)a.err, RLX_AGENT) != 0u) return;
+    const int2 task = a.tasks[tk];
+    const PairDesc pd = a.pairs[task.x];
+    const int band = task.y;
+    const int row0 = band * kBandRows + lane * kRows;  // 0-based first row of this lane
+    unsigned xq[kRows];
+    int h[kRows], e[kRows];
+    unsigned acc[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      const int row = row0 + r;
+      xq[r] = row < pd.m ? a.codes[pd.x_off + row] : 0x100u;
+      h[r] = go + (row + 1) * ge;  // H[i][0]
+      e[r] = kAffInf;              // E[i][0]
+      acc[r] = 0;
+    }
+    int Up = band == 0 ? 0 : go + band * kBandRows * ge;  // H[row above the band][0]
+    int f7 = kAffInf, stH = 0, stF = 0;
+
+    const bool from_above = band > 0;
+    const bool to_below = band + 1 < pd.nbands;
+    const int64_t bstride = (int64_t)pd.nchunks * 64;
+    const int64_t fbase = (int64_t)(pd.nbands - 1) * bstride;  // F rows follow the H rows
+    const int bin = band > 0 ? band - 1 : 0;
+    const u64* ginH = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)bin * bstride + lane;
+    const u64* ginF = ginH + fbase;
+    const int last_chunk = pd.nchunks > 0 ? pd.nchunks - 1 : 0;
+    u64* goutH = a.bnd + pd.bnd_off + (int64_t)band * bstride + lane;
+    u64* goutF = goutH + fbase;
+    unsigned* mptr = a.mat + pd.mat_off + (int64_t)band * band_dwords(W, pd.sblocks) + lane;
+    u64 pH = 0, pF = 0;
+    const unsigned* Ew = a.E + pd.e_off - 64 + lane;
+    unsigned ew0, ew1;
+    asm_load_E2(Ew, ew0, ew1);
+    asm_load_granule(ginH, pH);
+    asm_load_granule(ginF, pF);
+    wait_vm_keep4<0>(ew0, ew1, pH, pF);
+    bool ok = true;
+    constexpr int kBlockStores = kRows;
+
+    for (int sb = 0; sb < pd.sblocks; ++sb) {
+      PROG(0x20000000u | sb);
+      // --- band-above H and F rows for this super-block's columns 64sb+1 .. 64sb+64
+      int bh = go + (64 * sb + lane + 1) * ge, bf = kAffInf;  // band 0: H[0][j], F[0][j]
+      if (from_above) {
+        bh = 0;
+        if (sb < pd.nchunks) {
+          if (!__all((unsigned)(pH >> 32) == a.epoch)) pH = wait_granules(ginH + 64 * sb, a.epoch, pH, a.err);
+          if (!__all((unsigned)(pF >> 32) == a.epoch)) pF = wait_granules(ginF + 64 * sb, a.epoch, pF, a.err);
+          if (!__all((unsigned)(pH >> 32) == a.epoch && (unsigned)(pF >> 32) == a.epoch)) { ok = false; break; }
+          bh = (int)(unsigned)pH;
+          bf = (int)(unsigned)pF;
+        }
+      }
+      asm_load_granule(ginH + 64 * min(sb + 1, last_chunk), pH);
+      asm_load_granule(ginF + 64 * min(sb + 1, last_chunk), pF);
+      int* slH = ringH + (sb & 1) * 64;
+      int* slF = ringF + (sb & 1) * 64;
+      slH[lane] = bh;
+      slF[lane] = bf;
+      unsigned* ewin = ering + (sb & 1) * 128;
+      ewin[lane] = ew0;
+      ewin[64 + lane] = ew1;
+      asm_load_E2(Ew + 64 * (sb + 1), ew0, ew1);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (int blk = 0; blk < 8; ++blk) {
+        const int s0 = sb * 64 + blk * 8;
+        const unsigned e0 = ewin[blk * 8 + 64 - lane], e1 = ewin[blk * 8 + 68 - lane];
+        if (sb == 0)
+          step_block_affine<true>(s0, lane, h, e, Up, f7, stH, stF, acc, xq, e0, e1, slH + blk * 8, slF + blk * 8, mptr,
+                                  pxy, goe, ge);
+        else
+          step_block_affine<false>(s0, lane, h, e, Up, f7, stH, stF, acc, xq, e0, e1, slH + blk * 8, slF + blk * 8,
+                                   mptr, pxy, goe, ge);
+        mptr += (8 / SPD) * kRows * kWave;
+        wait_vm_keep4<kBlockStores>(ew0, ew1, pH, pF);
+      }
+      if (to_below && sb >= 1 && sb <= pd.nchunks) {
+        st_granule(goutH + 64 * (sb - 1), a.epoch, stH);
+        st_granule(goutF + 64 * (sb - 1), a.epoch, stF);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    PROG(0x30000000u);
+    if (!ok) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PROG(0x31000000u);
+    unsigned prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add((gu32*)(a.done + pd.slot), 1u, RLX_AGENT);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev + 1u == (unsigned)pd.nbands) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      PROG(0x40000000u);
+      if (a.dbg_notrace) {
+        if (lane == 0) { a.oplen[pd.slot] = 0; a.endij[pd.slot] = make_int2(pd.m, pd.n); }
+      } else {
+        trace_pair_affine(a, pd, tbl[wid], lane, prog);
+        PROG(0x56000000u);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 template <int MODE, int W>
 static hipError_t fill_w(const FillArgs& a, int grid, hipStream_t s) {
@@ -622,6 +961,10 @@ static hipError_t fill_m(int bits, const FillArgs& a, int grid, hipStream_t s) {
 
 hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStream_t s) {
   switch (mode) {
+    case kAffine:
+      if (bits != 4) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(nw_align_affine, dim3(grid), dim3(256), 0, s, a);
+      return hipGetLastError();
     case kProfile: return fill_m<kProfile>(bits, a, grid, s);
     case kCompare: return fill_m<kCompare>(bits, a, grid, s);
     case kLiteral: return bits == 32 ? fill_w<kLiteral, 32>(a, grid, s) : hipErrorInvalidValue;
@@ -639,6 +982,12 @@ static int occ_w() {
 
 int fill_blocks_per_cu(int mode, int bits) {
   if (mode == kLiteral) return occ_w<kLiteral, 32>();
+  if (mode == kAffine) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&nw_align_affine), 256, 0) != hipSuccess)
+      return 1;
+    return n > 0 ? n : 1;
+  }
   const bool p = mode == kProfile;
   switch (bits) {
     case 4: return p ? occ_w<kProfile, 4>() : occ_w<kCompare, 4>();

@@ -24,6 +24,7 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <unistd.h>
 
 #include "../../include/nwk.h"
 #include "nwk_internal.h"
@@ -145,7 +146,7 @@ struct nwk_ctx {
   // batch buffers
   DevBuf d_work;                // matrices | boundary granules | op strings
   int64_t clean_b = 0;          // leading bytes of d_work holding only zeros / old-epoch granules
-  DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij, d_done, d_stamps;
+  DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij, d_done, d_stamps, d_prog;
   HostBuf h_tasks;
   HostBuf h_pairs[2], h_oplen[2], h_endij[2], h_ops[2];  // double-buffered: batch b+1 runs while b finalizes
 
@@ -299,7 +300,24 @@ struct Plan {
   int K0, K1;
 };
 
-int choose_plan(const nwk_ctx* c, int pxy, int pgap, Plan* pl) {
+// Scoring of a call: the reference's linear gaps (pxy, pgap), or the
+// build-defined affine variant (pxy, go, ge) of SURVEY §8 a9.
+struct Scoring {
+  int pxy, pgap;
+  bool affine;
+  int go, ge;
+};
+
+int choose_plan(const nwk_ctx* c, const Scoring& sc, Plan* pl) {
+  const int pxy = sc.pxy, pgap = sc.pgap;
+  if (sc.affine) {
+    pl->mode = kAffine;
+    pl->bits = 4;  // 4-bit traceback codes
+    pl->kind = 1;  // raw bytes (compare)
+    pl->K0 = 0;
+    pl->K1 = pxy;
+    return NWK_OK;
+  }
   if (pxy < 0 || pgap < 0) {
     pl->mode = kLiteral;
     pl->bits = 32;
@@ -318,11 +336,11 @@ int choose_plan(const nwk_ctx* c, int pxy, int pgap, Plan* pl) {
   return NWK_OK;
 }
 
-void footprint(PairWork* w, int bits) {
+void footprint(PairWork* w, int bits, bool affine) {
   const int64_t nb = ceil_div(w->m, kBandRows);
   const int64_t nch = ceil_div(w->n, 64);
   w->mat_dw = nb * band_dwords(bits, (int)(nch + 1));
-  w->bnd_gr = (nb - 1) * nch * 64;
+  w->bnd_gr = (nb - 1) * nch * 64 * (affine ? 2 : 1);  // affine: H and F boundary rows
   w->ops_b = round_up((int64_t)w->m + w->n, 16);
 }
 
@@ -333,19 +351,23 @@ struct Finalized {
   unsigned char hash[64];
 };
 
-void finalize_pair(const uint8_t* x, int m, const uint8_t* y, int n, int pxy, int pgap,
+void finalize_pair(const uint8_t* x, int m, const uint8_t* y, int n, const Scoring& sc,
                    const uint8_t* ops_rev, int nops, int ei, int ej, Finalized* out,
                    std::vector<uint8_t>* a1o = nullptr, std::vector<uint8_t>* a2o = nullptr) {
   const int64_t L0 = (int64_t)(ei > 0 ? ei : ej) + nops;
   std::vector<uint8_t> a1((size_t)L0), a2((size_t)L0);
+  const int64_t pxy = sc.pxy;
+  // linear: every gap column costs pgap; affine: a gap's first column costs
+  // go + ge ('u'/'l' from the traceback, and the prefix run), the others ge
+  const int64_t gopen = sc.affine ? (int64_t)sc.go + sc.ge : sc.pgap, gext = sc.affine ? sc.ge : sc.pgap;
   int64_t pen = 0;
   int64_t q = 0;
   if (ei > 0) {
     for (int t = 0; t < ei; ++t, ++q) { a1[q] = x[t]; a2[q] = '_'; }
-    pen += (int64_t)ei * pgap;
+    pen += gopen + (int64_t)(ei - 1) * gext;
   } else if (ej > 0) {
     for (int t = 0; t < ej; ++t, ++q) { a1[q] = '_'; a2[q] = y[t]; }
-    pen += (int64_t)ej * pgap;
+    pen += gopen + (int64_t)(ej - 1) * gext;
   }
   int i = ei, j = ej;
   for (int t = nops - 1; t >= 0; --t, ++q) {
@@ -354,13 +376,13 @@ void finalize_pair(const uint8_t* x, int m, const uint8_t* y, int n, int pxy, in
       a1[q] = x[i]; a2[q] = y[j];
       pen += x[i] == y[j] ? 0 : pxy;
       ++i; ++j;
-    } else if (op == 'U') {
+    } else if (op == 'U' || op == 'u') {
       a1[q] = x[i]; a2[q] = '_';
-      pen += pgap;
+      pen += op == 'u' ? gopen : gext;
       ++i;
     } else {
       a1[q] = '_'; a2[q] = y[j];
-      pen += pgap;
+      pen += op == 'l' ? gopen : gext;
       ++j;
     }
   }
@@ -402,12 +424,20 @@ void parallel_for(int threads, int64_t n, F&& f) {
 
 // Core: aligns `work` (any order) and writes penalties/hashes at work[].out.
 // If strings != nullptr (single-pair API), also returns the alignment rows.
-int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32_t* penalties,
+int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32_t* penalties,
                uint8_t* hashes, std::vector<uint8_t>* a1, std::vector<uint8_t>* a2) {
   const double t_start = now_ms();
   nwk_stats st{};
   Plan pl;
-  choose_plan(c, pxy, pgap, &pl);
+  choose_plan(c, sc, &pl);
+  if (sc.affine) {
+    if (sc.pxy < 0 || sc.go < 0 || sc.ge < 0)
+      return fail(NWK_EINVAL, "affine gaps need pxy, go, ge >= 0 (got %d, %d, %d)", sc.pxy, sc.go, sc.ge);
+    // H values stay below the kernel's +inf (2^30 - 1) with room for one step
+    for (const auto& w : work)
+      if (((int64_t)w.m + w.n + 2) * ((int64_t)sc.go + sc.ge + sc.pxy) >= (1ll << 29))
+        return fail(NWK_EINVAL, "affine scores of pair (%d x %d) would exceed the int32 range", w.m, w.n);
+  }
   st.bits = pl.bits;
   st.mode = pl.mode;
   int rc;
@@ -422,11 +452,11 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
       Finalized f;
       const uint8_t* x = c->seqs.data() + c->off[w.i];
       const uint8_t* y = c->seqs.data() + c->off[w.j];
-      finalize_pair(x, w.m, y, w.n, pxy, pgap, nullptr, 0, w.m, w.n, &f, a1, a2);
+      finalize_pair(x, w.m, y, w.n, sc, nullptr, 0, w.m, w.n, &f, a1, a2);
       penalties[w.out] = f.penalty;
       memcpy(hashes + 64 * w.out, f.hash, 64);
     } else {
-      footprint(&w, pl.bits);
+      footprint(&w, pl.bits, sc.affine);
       dp.push_back(w);
     }
   }
@@ -559,6 +589,15 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     if (fa.epoch == 0) fa.epoch = ++c->epoch;
     fa.K0 = pl.K0;
     fa.K1 = pl.K1;
+    fa.go = sc.go;
+    fa.dbg_notrace = getenv("NWK_AFF_NOTRACE") ? 1 : 0;
+    fa.prog = nullptr;
+    if (getenv("NWK_WATCHDOG")) {
+      if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;
+      HIP_TRY(hipMemsetAsync(c->d_prog.p, 0, 4 * (size_t)(grid + 1) * 4, c->stream));
+      fa.prog = c->d_prog.as<unsigned>();
+    }
+    fa.ge = sc.ge;
     fa.stamps = nullptr;
     fa.ntasks_pairs = np;
     if (c->opts.verbose >= 2) {
@@ -580,6 +619,27 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(launch_fill(pl.mode, pl.bits, fa, std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    if (c->opts.verbose >= 3) {
+      fprintf(stderr, "nwk batch %d: launched mode %d bits %d grid %d, waiting\n", st.batches, pl.mode, pl.bits, grid);
+      fflush(stderr);
+    }
+    static const int watchdog = getenv("NWK_WATCHDOG") ? atoi(getenv("NWK_WATCHDOG")) : 0;
+    if (watchdog > 0) {  // debug: report where a launch that does not finish is stuck, then exit
+      const double t0 = now_ms();
+      while (hipStreamQuery(c->stream) == hipErrorNotReady && now_ms() - t0 < watchdog * 1000.0) usleep(10000);
+      if (hipStreamQuery(c->stream) == hipErrorNotReady) {
+        std::vector<unsigned> pg(4 * (size_t)(grid + 1));
+        hipStream_t s2;
+        (void)hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+        (void)hipMemcpyAsync(pg.data(), fa.prog, 4 * pg.size(), hipMemcpyDeviceToHost, s2);
+        (void)hipStreamSynchronize(s2);
+        fprintf(stderr, "nwk watchdog: launch still running after %d s; wave markers:\n", watchdog);
+        for (size_t q = 0; q < pg.size(); ++q)
+          if (pg[q]) fprintf(stderr, "  wave %zu: %08x\n", q, pg[q]);
+        fflush(stderr);
+        _exit(3);
+      }
+    }
     unsigned herr = 0;
     HIP_TRY(hipMemcpyAsync(&herr, fa.err, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_oplen[par].p, fa.oplen, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
@@ -639,12 +699,12 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, int pxy, int pgap, int32
     const int2* ej = c->h_endij[par].as<int2>();
     const uint8_t* hops = c->h_ops[par].as<uint8_t>();
     const PairWork* dw = dp.data() + pos;
-    auto job = [c, a1, a2, np, dw, pd, ol, ej, hops, ops_base_b, pxy, pgap, penalties, hashes]() {
+    auto job = [c, a1, a2, np, dw, pd, ol, ej, hops, ops_base_b, sc, penalties, hashes]() {
       parallel_for(a1 ? 1 : c->host_threads, np, [&](int64_t q) {
         const PairWork& w = dw[q];
         const PairDesc& d = pd[q];
         Finalized f;
-        finalize_pair(c->seqs.data() + c->off[w.i], w.m, c->seqs.data() + c->off[w.j], w.n, pxy, pgap,
+        finalize_pair(c->seqs.data() + c->off[w.i], w.m, c->seqs.data() + c->off[w.j], w.n, sc,
                       hops + (d.ops_off - ops_base_b), ol[q], ej[q].x, ej[q].y, &f, a1, a2);
         penalties[w.out] = f.penalty;
         memcpy(hashes + 64 * w.out, f.hash, 64);
@@ -685,14 +745,24 @@ int make_work(const nwk_ctx* c, const int64_t* ids, int64_t n, std::vector<PairW
 
 extern "C" {
 
-int nwk_align_pairs(nwk_ctx* c, const int64_t* pair_ids, int64_t npairs, int32_t pxy, int32_t pgap,
-                    int32_t* penalties, uint8_t* problem_hash) {
+static int align_pairs_sc(nwk_ctx* c, const int64_t* pair_ids, int64_t npairs, const Scoring& sc,
+                          int32_t* penalties, uint8_t* problem_hash) {
   if (!c || npairs < 0 || (npairs > 0 && (!pair_ids || !penalties || !problem_hash)))
     return fail(NWK_EINVAL, "nwk_align_pairs: bad argument");
   std::vector<PairWork> w;
   int rc = make_work(c, pair_ids, npairs, &w);
   if (rc != NWK_OK) return rc;
-  return align_work(c, w, pxy, pgap, penalties, problem_hash, nullptr, nullptr);
+  return align_work(c, w, sc, penalties, problem_hash, nullptr, nullptr);
+}
+
+int nwk_align_pairs(nwk_ctx* c, const int64_t* pair_ids, int64_t npairs, int32_t pxy, int32_t pgap,
+                    int32_t* penalties, uint8_t* problem_hash) {
+  return align_pairs_sc(c, pair_ids, npairs, Scoring{pxy, pgap, false, 0, 0}, penalties, problem_hash);
+}
+
+int nwk_align_pairs_affine(nwk_ctx* c, const int64_t* pair_ids, int64_t npairs, int32_t pxy, int32_t go,
+                           int32_t ge, int32_t* penalties, uint8_t* problem_hash) {
+  return align_pairs_sc(c, pair_ids, npairs, Scoring{pxy, 0, true, go, ge}, penalties, problem_hash);
 }
 
 int nwk_last_stats(const nwk_ctx* c, nwk_stats* out) {
@@ -701,8 +771,8 @@ int nwk_last_stats(const nwk_ctx* c, nwk_stats* out) {
   return NWK_OK;
 }
 
-int nwk_get_minimum_penalty(nwk_ctx* c, const uint8_t* x, int32_t m, const uint8_t* y, int32_t n, int32_t pxy,
-                            int32_t pgap, uint8_t* a1, uint8_t* a2, int32_t* alen, int32_t* penalty) {
+static int min_penalty_sc(nwk_ctx* c, const uint8_t* x, int32_t m, const uint8_t* y, int32_t n, const Scoring& sc,
+                          uint8_t* a1, uint8_t* a2, int32_t* alen, int32_t* penalty) {
   if (!c || m < 0 || n < 0 || (m && !x) || (n && !y) || !a1 || !a2 || !alen || !penalty)
     return fail(NWK_EINVAL, "nwk_get_minimum_penalty: bad argument");
   // set {y, x}: pair 0 = (i=1 -> rows x, j=0 -> columns y)
@@ -717,11 +787,21 @@ int nwk_get_minimum_penalty(nwk_ctx* c, const uint8_t* x, int32_t m, const uint8
   if ((rc = make_work(c, &id, 1, &w)) != NWK_OK) return rc;
   std::vector<uint8_t> r1, r2;
   unsigned char h[64];
-  if ((rc = align_work(c, w, pxy, pgap, penalty, h, &r1, &r2)) != NWK_OK) return rc;
+  if ((rc = align_work(c, w, sc, penalty, h, &r1, &r2)) != NWK_OK) return rc;
   memcpy(a1, r1.data(), r1.size());
   memcpy(a2, r2.data(), r2.size());
   *alen = (int32_t)r1.size();
   return NWK_OK;
+}
+
+int nwk_get_minimum_penalty(nwk_ctx* c, const uint8_t* x, int32_t m, const uint8_t* y, int32_t n, int32_t pxy,
+                            int32_t pgap, uint8_t* a1, uint8_t* a2, int32_t* alen, int32_t* penalty) {
+  return min_penalty_sc(c, x, m, y, n, Scoring{pxy, pgap, false, 0, 0}, a1, a2, alen, penalty);
+}
+
+int nwk_get_minimum_penalty_affine(nwk_ctx* c, const uint8_t* x, int32_t m, const uint8_t* y, int32_t n, int32_t pxy,
+                                   int32_t go, int32_t ge, uint8_t* a1, uint8_t* a2, int32_t* alen, int32_t* penalty) {
+  return min_penalty_sc(c, x, m, y, n, Scoring{pxy, 0, true, go, ge}, a1, a2, alen, penalty);
 }
 
 int nwk_shard_pairs(const int64_t* offsets, int32_t k, int32_t rank, int32_t world, int64_t* out_ids,
@@ -785,8 +865,8 @@ struct ResultRecord {
 };
 static_assert(sizeof(ResultRecord) == 72, "record layout");
 
-int nwk_get_minimum_penalties(const uint8_t* seqs, const int64_t* offsets, int32_t k, int32_t pxy, int32_t pgap,
-                              int32_t* penalties, char* hash_hex, const nwk_opts* opts) {
+static int min_penalties_sc(const uint8_t* seqs, const int64_t* offsets, int32_t k, const Scoring& sc,
+                            int32_t* penalties, char* hash_hex, const nwk_opts* opts) {
   if (k < 0 || !hash_hex || (k > 0 && !offsets)) return fail(NWK_EINVAL, "nwk_get_minimum_penalties: bad argument");
   nwk_opts o;
   nwk_opts_default(&o);
@@ -806,7 +886,7 @@ int nwk_get_minimum_penalties(const uint8_t* seqs, const int64_t* offsets, int32
     std::vector<int64_t> ids((size_t)P);
     for (int64_t p = 0; p < P; ++p) ids[p] = p;
     rc = nwk_set_sequences(c, seqs, offsets, k);
-    if (rc == NWK_OK) rc = nwk_align_pairs(c, ids.data(), P, pxy, pgap, penalties, ph.data());
+    if (rc == NWK_OK) rc = align_pairs_sc(c, ids.data(), P, sc, penalties, ph.data());
     nwk_ctx_destroy(c);
     if (rc != NWK_OK) return rc;
     return nwk_chain_hash(ph.data(), P, hash_hex);
@@ -843,7 +923,7 @@ int nwk_get_minimum_penalties(const uint8_t* seqs, const int64_t* offsets, int32
       if (rc == NWK_OK) rc = nwk_set_sequences(c, seqs, offsets, k);
       std::vector<int32_t> pen((size_t)std::max<int64_t>(n, 1));
       std::vector<uint8_t> hh((size_t)std::max<int64_t>(n, 1) * 64);
-      if (rc == NWK_OK && n > 0) rc = nwk_align_pairs(c, shard[r].data(), n, pxy, pgap, pen.data(), hh.data());
+      if (rc == NWK_OK && n > 0) rc = align_pairs_sc(c, shard[r].data(), n, sc, pen.data(), hh.data());
       for (int64_t q = 0; rc == NWK_OK && q < n; ++q) {
         rec[q].pair_id = (int32_t)shard[r][q];
         rec[q].penalty = pen[q];
@@ -889,6 +969,16 @@ int nwk_get_minimum_penalties(const uint8_t* seqs, const int64_t* offsets, int32
   for (int64_t p = 0; p < P; ++p)
     if (!have[p]) return fail(NWK_ECOMM, "pair %lld missing after all-gather", (long long)p);
   return nwk_chain_hash(ph.data(), P, hash_hex);
+}
+
+int nwk_get_minimum_penalties(const uint8_t* seqs, const int64_t* offsets, int32_t k, int32_t pxy, int32_t pgap,
+                              int32_t* penalties, char* hash_hex, const nwk_opts* opts) {
+  return min_penalties_sc(seqs, offsets, k, Scoring{pxy, pgap, false, 0, 0}, penalties, hash_hex, opts);
+}
+
+int nwk_get_minimum_penalties_affine(const uint8_t* seqs, const int64_t* offsets, int32_t k, int32_t pxy, int32_t go,
+                                     int32_t ge, int32_t* penalties, char* hash_hex, const nwk_opts* opts) {
+  return min_penalties_sc(seqs, offsets, k, Scoring{pxy, 0, true, go, ge}, penalties, hash_hex, opts);
 }
 
 }  // extern "C"

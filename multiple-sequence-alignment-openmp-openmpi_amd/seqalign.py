@@ -23,7 +23,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libnwk.so")
 
 NWK_OK = 0
 ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "EKERNEL", -5: "ECOMM"}
-MODES = {0: "profile", 1: "compare", 2: "literal"}
+MODES = {0: "profile", 1: "compare", 2: "literal", 3: "affine"}
 
 
 class NwkError(RuntimeError):
@@ -60,6 +60,9 @@ SIGNATURES = {
     "nwk_last_stats": (ctypes.c_int, [_P, _P]),
     "nwk_get_minimum_penalties": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P]),
     "nwk_get_minimum_penalty": (ctypes.c_int, [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
+    "nwk_align_pairs_affine": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _I32, _P, _P]),
+    "nwk_get_minimum_penalty_affine": (ctypes.c_int, [_P, _P, _I32, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),
+    "nwk_get_minimum_penalties_affine": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P]),
     "nwk_shard_pairs": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
     "nwk_chain_hash": (ctypes.c_int, [_P, _I64, _P]),
     "nwk_sha512_hex": (None, [_P, _I64, _P]),
@@ -175,6 +178,26 @@ class Engine:
         _check(self.lib.nwk_align_pairs(self._ctx, _ptr(ids), n, pxy, pgap, _ptr(pen), _ptr(hs)))
         return pen[:n], hs[:n]
 
+    def align_pairs_affine(self, pair_ids, pxy, go, ge):
+        """Affine-gap variant of align_pairs."""
+        ids = np.ascontiguousarray(pair_ids, dtype=np.int64)
+        n = ids.size
+        pen = np.zeros(max(n, 1), dtype=np.int32)
+        hs = np.zeros((max(n, 1), 64), dtype=np.uint8)
+        _check(self.lib.nwk_align_pairs_affine(self._ctx, _ptr(ids), n, pxy, go, ge, _ptr(pen), _ptr(hs)))
+        return pen[:n], hs[:n]
+
+    def get_minimum_penalty_affine(self, x, y, pxy, go, ge):
+        xb, yb = _as_bytes(x), _as_bytes(y)
+        m, n = len(xb), len(yb)
+        a1 = ctypes.create_string_buffer(max(m + n, 1))
+        a2 = ctypes.create_string_buffer(max(m + n, 1))
+        alen, pen = ctypes.c_int32(), ctypes.c_int32()
+        _check(self.lib.nwk_get_minimum_penalty_affine(self._ctx, xb, m, yb, n, pxy, go, ge, a1, a2,
+                                                       ctypes.byref(alen), ctypes.byref(pen)))
+        self.k = 2
+        return pen.value, a1.raw[:alen.value], a2.raw[:alen.value]
+
     def stats(self):
         s = Stats()
         _check(self.lib.nwk_last_stats(self._ctx, ctypes.byref(s)))
@@ -236,6 +259,24 @@ def getMinimumPenalties(genes, k, pxy, pgap, penalties, ngpus=1, bits=0, verbose
     o.ngpus, o.bits, o.verbose = ngpus, bits, int(verbose)
     _check(lib.nwk_get_minimum_penalties(_ptr(data), _ptr(offs), k, pxy, pgap, _ptr(pen), out,
                                          ctypes.byref(o)))
+    for p in range(P):
+        penalties[p] = int(pen[p])
+    return out.value.decode()
+
+
+def getMinimumPenaltiesAffine(genes, k, pxy, go, ge, penalties, ngpus=1, verbose=False):
+    """Affine-gap variant of getMinimumPenalties (go=0, ge=pgap == linear)."""
+    lib = load_library()
+    genes = list(genes)[:k]
+    data, offs = pack_genes(genes)
+    P = k * (k - 1) // 2
+    pen = np.zeros(max(P, 1), dtype=np.int32)
+    out = ctypes.create_string_buffer(129)
+    o = Opts()
+    lib.nwk_opts_default(ctypes.byref(o))
+    o.ngpus, o.verbose = ngpus, int(verbose)
+    _check(lib.nwk_get_minimum_penalties_affine(_ptr(data), _ptr(offs), k, pxy, go, ge, _ptr(pen), out,
+                                                ctypes.byref(o)))
     for p in range(P):
         penalties[p] = int(pen[p])
     return out.value.decode()

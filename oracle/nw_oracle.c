@@ -8,6 +8,9 @@
  *
  * What it restates (paths relative to the reference repository):
  *   nwo_pair()        seqalign-mpi-skeleton.cpp:186-280  getMinimumPenalty
+ *   nwo_pair_affine() the build-defined affine-gap variant (SURVEY.md §8 a9;
+ *                     no reference counterpart -- pinned only through its
+ *                     degenerate case go=0, ge=pgap == nwo_pair)
  *                       fill 211-226, traceback 236-262, prefix 263-272
  *                     + seqalign-mpi-skeleton.cpp:135-154 trim / build strings
  *   nwo_problem_hash  seqalign-mpi-skeleton.cpp:155-157 (sha512 of the two
@@ -178,6 +181,87 @@ int nwo_pair(const unsigned char *x, int m, const unsigned char *y, int n, int p
     if ((char)yans[a] == '_' && (char)xans[a] == '_') { id = a + 1; break; }
   }
   /* skel:145-154 */
+  int L = 0;
+  for (int a = id; a <= l; a++, L++) {
+    a1[L] = (unsigned char)xans[a];
+    a2[L] = (unsigned char)yans[a];
+  }
+  *alen = L;
+  free(xans); free(yans);
+  return ret;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Affine-gap variant.  NOT in the reference: the build     */
+/* defines it, so only its degenerate case go = 0, ge = pgap is pinned (it   */
+/* must reproduce nwo_pair, and with it every linear golden vector).         */
+/*   E[i][j] = min(E[i][j-1] + ge, H[i][j-1] + go + ge)        (LEFT)         */
+/*   F[i][j] = min(F[i-1][j] + ge, H[i-1][j] + go + ge)        (UP)           */
+/*   H[i][j] = x == y ? H[i-1][j-1] : min(H[i-1][j-1] + pxy, F, E)           */
+/*   H[0][0] = 0, H[i][0] = go + i ge, H[0][j] = go + j ge, E[i][0] = F[0][j] */
+/*   = +inf.  Traceback from (m, n) in state H: DIAG on a match, DIAG if     */
+/*   H[i-1][j-1] + pxy == H, else F if F == H, else E; in state F (E) emit   */
+/*   UP (LEFT) and return to H when the open term equals F (E) -- open wins  */
+/*   ties -- else stay.  Prefix fill and trim as skel:263-272, 135-154.      */
+/* ------------------------------------------------------------------------ */
+#define NWO_INF 0x3fffffff
+
+int nwo_pair_affine(const unsigned char *x, int m, const unsigned char *y, int n, int pxy, int go,
+                    int ge, unsigned char *a1, unsigned char *a2, int *alen) {
+  size_t W = (size_t)n + 1, N = (size_t)(m + 1) * W;
+  int *H = (int *)malloc(sizeof(int) * N), *E = (int *)malloc(sizeof(int) * N), *F = (int *)malloc(sizeof(int) * N);
+  int l = m + n;
+  int *xans = (int *)malloc(sizeof(int) * (size_t)(l + 1)), *yans = (int *)malloc(sizeof(int) * (size_t)(l + 1));
+  if (!H || !E || !F || !xans || !yans) {
+    free(H); free(E); free(F); free(xans); free(yans);
+    return INT32_MIN;
+  }
+#define AT(A, i, j) A[(size_t)(i) * W + (size_t)(j)]
+  AT(H, 0, 0) = 0;
+  AT(E, 0, 0) = AT(F, 0, 0) = NWO_INF;
+  for (int i = 1; i <= m; ++i) { AT(H, i, 0) = go + i * ge; AT(E, i, 0) = NWO_INF; AT(F, i, 0) = NWO_INF; }
+  for (int j = 1; j <= n; ++j) { AT(H, 0, j) = go + j * ge; AT(F, 0, j) = NWO_INF; AT(E, 0, j) = NWO_INF; }
+  for (int i = 1; i <= m; ++i)
+    for (int j = 1; j <= n; ++j) {
+      int eo = AT(H, i, j - 1) + go + ge, ee = AT(E, i, j - 1) + ge;
+      int fo = AT(H, i - 1, j) + go + ge, fe = AT(F, i - 1, j) + ge;
+      int e = eo < ee ? eo : ee, f = fo < fe ? fo : fe;
+      AT(E, i, j) = e;
+      AT(F, i, j) = f;
+      if (x[i - 1] == y[j - 1]) {
+        AT(H, i, j) = AT(H, i - 1, j - 1);
+      } else {
+        int h = AT(H, i - 1, j - 1) + pxy;
+        if (f < h) h = f;
+        if (e < h) h = e;
+        AT(H, i, j) = h;
+      }
+    }
+  int i = m, j = n, xpos = l, ypos = l, st = 0; /* 0 = H, 1 = F, 2 = E */
+  while (!(i == 0 || j == 0)) {
+    if (st == 0) {
+      if (x[i - 1] == y[j - 1] || AT(H, i - 1, j - 1) + pxy == AT(H, i, j)) {
+        xans[xpos--] = x[i - 1]; yans[ypos--] = y[j - 1]; i--; j--;
+        continue;
+      }
+      st = AT(F, i, j) == AT(H, i, j) ? 1 : 2;
+    }
+    if (st == 1) {
+      st = AT(H, i - 1, j) + go + ge == AT(F, i, j) ? 0 : 1;
+      xans[xpos--] = x[i - 1]; yans[ypos--] = '_'; i--;
+    } else {
+      st = AT(H, i, j - 1) + go + ge == AT(E, i, j) ? 0 : 2;
+      xans[xpos--] = '_'; yans[ypos--] = y[j - 1]; j--;
+    }
+  }
+  while (xpos > 0) { if (i > 0) xans[xpos--] = x[--i]; else xans[xpos--] = '_'; }
+  while (ypos > 0) { if (j > 0) yans[ypos--] = y[--j]; else yans[ypos--] = '_'; }
+  int ret = AT(H, m, n);
+#undef AT
+  free(H); free(E); free(F);
+  int id = 1;
+  for (int a = l; a >= 1; a--)
+    if ((char)yans[a] == '_' && (char)xans[a] == '_') { id = a + 1; break; }
   int L = 0;
   for (int a = id; a <= l; a++, L++) {
     a1[L] = (unsigned char)xans[a];

@@ -32,6 +32,8 @@ def lib():
         P = ctypes.c_void_p
         L.nwo_pair.restype = ctypes.c_int
         L.nwo_pair.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P]
+        L.nwo_pair_affine.restype = ctypes.c_int
+        L.nwo_pair_affine.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P]
         L.nwo_problem_hash.restype = None
         L.nwo_problem_hash.argtypes = [P, P, ctypes.c_int, P]
         L.nwo_chain.restype = None
@@ -59,6 +61,30 @@ def pair(x, y, pxy, pgap):
     if pen == -2 ** 31:
         raise MemoryError("oracle: DP allocation failed")
     return pen, a1.raw[:alen.value], a2.raw[:alen.value]
+
+
+def pair_affine(x, y, pxy, go, ge):
+    """Affine-gap variant (build-defined): (penalty, align1, align2)."""
+    x, y = _b(x), _b(y)
+    cap = max(len(x) + len(y), 1)
+    a1 = ctypes.create_string_buffer(cap)
+    a2 = ctypes.create_string_buffer(cap)
+    alen = ctypes.c_int()
+    pen = lib().nwo_pair_affine(x, len(x), y, len(y), pxy, go, ge, a1, a2, ctypes.byref(alen))
+    if pen == -2 ** 31:
+        raise MemoryError("oracle: DP allocation failed")
+    return pen, a1.raw[:alen.value], a2.raw[:alen.value]
+
+
+def all_pairs_affine(genes, pxy, go, ge):
+    """(hash, penalties, per-pair problemhash hex) of the affine variant, canonical order."""
+    pens, hs = [], []
+    for i in range(1, len(genes)):
+        for j in range(i):
+            p, a1, a2 = pair_affine(genes[i], genes[j], pxy, go, ge)
+            pens.append(p)
+            hs.append(problem_hash(a1, a2))
+    return chain(hs), pens, hs
 
 
 def problem_hash(a1, a2):

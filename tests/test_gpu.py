@@ -180,3 +180,62 @@ def test_sharded_union_equals_unsharded(engine, golden):
         pen[ids] = p
         hs[ids] = h
     assert seqalign.chain_hash(hs) == golden["xulin_test"]["hash"]
+
+
+# ---------------------------------------------------------------------------
+# Affine-gap variant.  Pinned to the reference only through
+# go=0, ge=pgap (must reproduce every linear golden vector, big13 included);
+# go > 0 is checked bit-exact against the oracle's restatement (parity
+# unpinned by the reference).
+# ---------------------------------------------------------------------------
+AFFINE_GOLDEN = [c for c in GOLDEN if min(case_input(c)[:2]) >= 0]
+
+
+@pytest.mark.parametrize("case", AFFINE_GOLDEN, ids=[c["name"] for c in AFFINE_GOLDEN])
+def test_affine_degenerate_golden(engine, case):
+    pxy, pgap, genes = case_input(case)
+    engine.set_sequences(genes)
+    pen, hs = engine.align_pairs_affine(_all_ids(len(genes)), pxy, 0, pgap)
+    assert [int(v) for v in pen] == case["penalties"]
+    assert seqalign.chain_hash(hs) == case["hash"]
+
+
+AFFINE_PARAMS = [(3, 4, 1), (1, 2, 2), (0, 5, 0), (7, 0, 3), (4, 10, 1), (2, 1, 1)]
+
+
+@pytest.mark.parametrize("pxy,go,ge", AFFINE_PARAMS)
+def test_affine_random_vs_oracle(engine, pxy, go, ge):
+    r = random.Random(pxy * 100 + go * 10 + ge)
+    genes = _rand_genes(r, 5, 1, 700, ACGT) + _mutants(r, bytes(r.choice(ACGT) for _ in range(650)), 3, ACGT)
+    genes += [bytes(r.choice(b"AC_x") for _ in range(L)) for L in (63, 64, 65, 511, 512, 513)]
+    engine.set_sequences(genes)
+    pen, hs = engine.align_pairs_affine(_all_ids(len(genes)), pxy, go, ge)
+    h, opens, ohs = oracle.all_pairs_affine(genes, pxy, go, ge)
+    assert [int(v) for v in pen] == opens
+    assert [x.tobytes().hex() for x in hs] == ohs
+    assert seqalign.chain_hash(hs) == h
+
+
+@pytest.mark.parametrize("m,n", [(1, 1), (1, 9), (9, 1), (700, 30), (30, 700), (1100, 1030), (2000, 64)])
+def test_affine_single_pair_strings(engine, m, n):
+    r = random.Random(m * 7 + n)
+    x = bytes(r.choice(ACGT) for _ in range(m))
+    y = bytes(r.choice(ACGT) for _ in range(n))
+    for pxy, go, ge in ((3, 4, 1), (2, 0, 2), (5, 8, 0)):
+        assert engine.get_minimum_penalty_affine(x, y, pxy, go, ge) == oracle.pair_affine(x, y, pxy, go, ge)
+
+
+def test_affine_multi_batch_and_api(golden):
+    r = random.Random(21)
+    genes = _rand_genes(r, 7, 600, 1300, ACGT)
+    with seqalign.Engine(device=0, workspace_bytes=3 << 20) as e:
+        e.set_sequences(genes)
+        pen, hs = e.align_pairs_affine(_all_ids(len(genes)), 3, 4, 1)
+        st = e.stats()
+        assert st["batches"] > 1 and st["mode"] == 3
+    h, opens, ohs = oracle.all_pairs_affine(genes, 3, 4, 1)
+    assert [int(v) for v in pen] == opens and [x.tobytes().hex() for x in hs] == ohs
+    pens = [0] * len(opens)
+    assert seqalign.getMinimumPenaltiesAffine(genes, len(genes), 3, 4, 1, pens) == h and pens == opens
+    with pytest.raises(seqalign.NwkError):
+        seqalign.getMinimumPenaltiesAffine(genes, len(genes), -1, 4, 1, pens)
