@@ -18,8 +18,16 @@ for d in libs * int(os.environ.get("ROUNDS", "1")):
     ids = np.arange(78, dtype=np.int64)
     ks, ws = [], []
     for r in range(reps):
-        t0 = time.perf_counter(); pen, hs = e.align_pairs(ids, pxy, pgap); ws.append(time.perf_counter() - t0)
-        assert seqalign.chain_hash(hs) == GOLD, "big13 hash mismatch"
+        aff = os.environ.get("AFF")  # "go,ge": affine variant (no golden check unless go == 0, ge == pgap)
+        t0 = time.perf_counter()
+        if aff:
+            go, ge = (int(v) for v in aff.split(","))
+            pen, hs = e.align_pairs_affine(ids, pxy, go, ge)
+        else:
+            pen, hs = e.align_pairs(ids, pxy, pgap)
+        ws.append(time.perf_counter() - t0)
+        if not aff or aff == "0,%d" % pgap:
+            assert seqalign.chain_hash(hs) == GOLD, "big13 hash mismatch"
         ks.append(e.stats()["fill_ms"])
     e.close()
     print("timeit %-40s kernel ms min %.2f med %.2f | wall ms min %.2f med %.2f" % (d, min(ks), sorted(ks)[len(ks)//2], 1e3*min(ws), 1e3*sorted(ws)[len(ws)//2]), flush=True)
