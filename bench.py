@@ -149,17 +149,27 @@ def main():
     import seqalign
 
     dist = None
+    coll_device = None
+    gpu = local
     if world > 1:
         import torch
         import torch.distributed as tdist
 
         import dist as nwdist
 
-        torch.cuda.set_device(local)
+        # Test hooks (not used by the driver): NWK_BENCH_BACKEND=gloo and
+        # NWK_BENCH_SHARE_GPU=1 rehearse the N-rank path on a 1-GPU box.
+        backend = os.environ.get("NWK_BENCH_BACKEND", "nccl")
+        if os.environ.get("NWK_BENCH_SHARE_GPU") == "1":
+            gpu = local % max(1, seqalign.device_count())
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.cuda.set_device(gpu)
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            coll_device = torch.device("cuda", gpu)
+        else:
+            tdist.init_process_group(backend)
         dist = tdist
-        device = torch.device("cuda", local)
 
     name, pxy, pgap, genes, gold_hash = load_workload(args.workload)
     affine = args.affine if args.affine is not None else ("3,1" if args.workload == "c5" else None)
@@ -171,7 +181,8 @@ def main():
     P = k * (k - 1) // 2
     lengths = [len(g) for g in genes]
     total_cells = cells_of(genes, range(P))
-    eng = seqalign.Engine(device=local if world > 1 else 0, bits=args.bits, verbose=args.verbose)
+    ws = int(float(os.environ.get("NWK_BENCH_WS_GB", "0")) * (1 << 30))  # test hook: per-rank HBM budget
+    eng = seqalign.Engine(device=gpu if world > 1 else 0, bits=args.bits, verbose=args.verbose, workspace_bytes=ws)
     eng.set_sequences(genes)  # sequences resident in HBM before timing
     my_ids = seqalign.shard_pairs(lengths, rank, world) if world > 1 else np.arange(P, dtype=np.int64)
 
@@ -183,7 +194,7 @@ def main():
 
     def step():
         if world > 1:
-            pen, hs, _ = nwdist.align_sharded(align, lengths, pxy, pgap, rank, world, device=device)
+            pen, hs, _ = nwdist.align_sharded(align, lengths, pxy, pgap, rank, world, device=coll_device)
         else:
             pen, hs = align(my_ids, pxy, pgap)
         h = seqalign.chain_hash(hs) if rank == 0 else None
@@ -194,7 +205,8 @@ def main():
             import torch
 
             dist.barrier()
-            torch.cuda.synchronize()
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
 
     checked = None
     for _ in range(args.warmup):
@@ -216,7 +228,7 @@ def main():
     if world > 1:
         import torch
 
-        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     if rank != 0:
@@ -235,7 +247,7 @@ def main():
     achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_summary.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and world == 1 and not affine:  # measured for the N=1 linear launch
         try:
             traffic = json.load(open(pmc)).get(args.workload, {}).get("hbm_bytes_per_fill_launch")
         except Exception:
