@@ -195,9 +195,9 @@ def main():
     def step():
         if world > 1:
             pen, hs, _ = nwdist.align_sharded(align, lengths, pxy, pgap, rank, world, device=coll_device)
-        else:
-            pen, hs = align(my_ids, pxy, pgap)
-        h = seqalign.chain_hash(hs) if rank == 0 else None
+            h = seqalign.chain_hash(hs) if rank == 0 else None
+        else:  # getMinimumPenalties on the engine: the chain overlaps later batches
+            h, pen, _ = eng.align_all(pxy, pgap, affine=(go, ge) if affine else None)
         return pen, h
 
     def sync():

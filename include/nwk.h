@@ -101,6 +101,16 @@ int nwk_set_sequences(nwk_ctx *ctx, const uint8_t *seqs, const int64_t *offsets,
 int nwk_align_pairs(nwk_ctx *ctx, const int64_t *pair_ids, int64_t npairs, int32_t pxy,
                     int32_t pgap, int32_t *penalties, uint8_t *problem_hash);
 
+/*
+ * getMinimumPenalties on a context (skel:117-175, sub:232-364): aligns all
+ * P = k(k-1)/2 pairs of the current sequence set, fills penalties[P] (and
+ * problem_hash[P*64] unless NULL) in canonical order and writes the chained
+ * answer hash (skel:159) into hash_hex[129].  The chain runs on the host
+ * while later workspace batches are still on the GPU.
+ */
+int nwk_align_all(nwk_ctx *ctx, int32_t pxy, int32_t pgap, int32_t *penalties,
+                  uint8_t *problem_hash, char *hash_hex);
+
 /* Statistics of the context's last nwk_align_pairs call. */
 int nwk_last_stats(const nwk_ctx *ctx, nwk_stats *out);
 
@@ -141,6 +151,8 @@ int nwk_align_pairs_affine(nwk_ctx *ctx, const int64_t *pair_ids, int64_t npairs
 int nwk_get_minimum_penalty_affine(nwk_ctx *ctx, const uint8_t *x, int32_t m, const uint8_t *y,
                                    int32_t n, int32_t pxy, int32_t go, int32_t ge, uint8_t *a1,
                                    uint8_t *a2, int32_t *alen, int32_t *penalty);
+int nwk_align_all_affine(nwk_ctx *ctx, int32_t pxy, int32_t go, int32_t ge, int32_t *penalties,
+                         uint8_t *problem_hash, char *hash_hex);
 int nwk_get_minimum_penalties_affine(const uint8_t *seqs, const int64_t *offsets, int32_t k,
                                      int32_t pxy, int32_t go, int32_t ge, int32_t *penalties,
                                      char *hash_hex, const nwk_opts *opts);

@@ -424,8 +424,30 @@ void parallel_for(int threads, int64_t n, F&& f) {
 
 // Core: aligns `work` (any order) and writes penalties/hashes at work[].out.
 // If strings != nullptr (single-pair API), also returns the alignment rows.
+// The answer-hash chain of skel:159 advanced while later batches still run:
+// results are marked ready by output index (= canonical pair id for a full
+// call) and the chain consumes the ready prefix.
+struct Chain {
+  const uint8_t* hashes = nullptr;  // [P][64] raw problem hashes
+  std::vector<char> ready;
+  int64_t next = 0;
+  char buf[256];
+  size_t la = 0;  // acc starts as "" (skel:121)
+  void advance() {
+    const int64_t P = (int64_t)ready.size();
+    while (next < P && ready[next]) {
+      to_hex(hashes + 64 * next, buf + la);
+      char acc[128];
+      sha512_hex(buf, la + 128, acc);
+      memcpy(buf, acc, 128);
+      la = 128;
+      ++next;
+    }
+  }
+};
+
 int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32_t* penalties,
-               uint8_t* hashes, std::vector<uint8_t>* a1, std::vector<uint8_t>* a2) {
+               uint8_t* hashes, std::vector<uint8_t>* a1, std::vector<uint8_t>* a2, Chain* chain = nullptr) {
   const double t_start = now_ms();
   nwk_stats st{};
   Plan pl;
@@ -455,6 +477,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       finalize_pair(x, w.m, y, w.n, sc, nullptr, 0, w.m, w.n, &f, a1, a2);
       penalties[w.out] = f.penalty;
       memcpy(hashes + 64 * w.out, f.hash, 64);
+      if (chain) chain->ready[w.out] = 1;
     } else {
       footprint(&w, pl.bits, sc.affine);
       dp.push_back(w);
@@ -699,7 +722,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     const int2* ej = c->h_endij[par].as<int2>();
     const uint8_t* hops = c->h_ops[par].as<uint8_t>();
     const PairWork* dw = dp.data() + pos;
-    auto job = [c, a1, a2, np, dw, pd, ol, ej, hops, ops_base_b, sc, penalties, hashes]() {
+    auto job = [c, a1, a2, np, dw, pd, ol, ej, hops, ops_base_b, sc, penalties, hashes, chain]() {
       parallel_for(a1 ? 1 : c->host_threads, np, [&](int64_t q) {
         const PairWork& w = dw[q];
         const PairDesc& d = pd[q];
@@ -709,6 +732,10 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         penalties[w.out] = f.penalty;
         memcpy(hashes + 64 * w.out, f.hash, 64);
       });
+      if (chain) {  // serial: jobs never overlap each other (fin.join() before the next starts)
+        for (int64_t q = 0; q < np; ++q) chain->ready[dw[q].out] = 1;
+        chain->advance();
+      }
     };
     if (end < dp.size()) fin.start(job);
     else job();
@@ -763,6 +790,40 @@ int nwk_align_pairs(nwk_ctx* c, const int64_t* pair_ids, int64_t npairs, int32_t
 int nwk_align_pairs_affine(nwk_ctx* c, const int64_t* pair_ids, int64_t npairs, int32_t pxy, int32_t go,
                            int32_t ge, int32_t* penalties, uint8_t* problem_hash) {
   return align_pairs_sc(c, pair_ids, npairs, Scoring{pxy, 0, true, go, ge}, penalties, problem_hash);
+}
+
+static int align_all_sc(nwk_ctx* c, const Scoring& sc, int32_t* penalties, uint8_t* problem_hash, char* hash_hex) {
+  if (!c || !hash_hex) return fail(NWK_EINVAL, "nwk_align_all: bad argument");
+  const int64_t P = (int64_t)c->k * (c->k - 1) / 2;
+  if (P > 0 && !penalties) return fail(NWK_EINVAL, "nwk_align_all: penalties is NULL");
+  std::vector<uint8_t> own;
+  if (!problem_hash) {
+    own.resize((size_t)std::max<int64_t>(P, 1) * 64);
+    problem_hash = own.data();
+  }
+  std::vector<int64_t> ids((size_t)P);
+  for (int64_t p = 0; p < P; ++p) ids[p] = p;
+  std::vector<PairWork> w;
+  int rc = make_work(c, ids.data(), P, &w);
+  if (rc != NWK_OK) return rc;
+  Chain ch;
+  ch.hashes = problem_hash;
+  ch.ready.assign((size_t)P, 0);
+  if ((rc = align_work(c, w, sc, penalties, problem_hash, nullptr, nullptr, &ch)) != NWK_OK) return rc;
+  ch.advance();  // pairs with no DP cells, if they are the tail
+  if (ch.next != P) return fail(NWK_EKERNEL, "nwk_align_all: chain stopped at pair %lld of %lld", (long long)ch.next, (long long)P);
+  memcpy(hash_hex, ch.buf, ch.la);
+  hash_hex[ch.la] = 0;
+  return NWK_OK;
+}
+
+int nwk_align_all(nwk_ctx* c, int32_t pxy, int32_t pgap, int32_t* penalties, uint8_t* problem_hash, char* hash_hex) {
+  return align_all_sc(c, Scoring{pxy, pgap, false, 0, 0}, penalties, problem_hash, hash_hex);
+}
+
+int nwk_align_all_affine(nwk_ctx* c, int32_t pxy, int32_t go, int32_t ge, int32_t* penalties, uint8_t* problem_hash,
+                         char* hash_hex) {
+  return align_all_sc(c, Scoring{pxy, 0, true, go, ge}, penalties, problem_hash, hash_hex);
 }
 
 int nwk_last_stats(const nwk_ctx* c, nwk_stats* out) {
@@ -883,13 +944,10 @@ static int min_penalties_sc(const uint8_t* seqs, const int64_t* offsets, int32_t
     nwk_ctx* c = nullptr;
     int rc = nwk_ctx_create(&o, &c);
     if (rc != NWK_OK) return rc;
-    std::vector<int64_t> ids((size_t)P);
-    for (int64_t p = 0; p < P; ++p) ids[p] = p;
     rc = nwk_set_sequences(c, seqs, offsets, k);
-    if (rc == NWK_OK) rc = align_pairs_sc(c, ids.data(), P, sc, penalties, ph.data());
+    if (rc == NWK_OK) rc = align_all_sc(c, sc, penalties, ph.data(), hash_hex);
     nwk_ctx_destroy(c);
-    if (rc != NWK_OK) return rc;
-    return nwk_chain_hash(ph.data(), P, hash_hex);
+    return rc;
   }
   if (G > nwk_device_count()) return fail(NWK_EINVAL, "ngpus=%d > visible devices %d", G, nwk_device_count());
   // Shards: LPT on cell cost; every rank sends a padded block of `per` records.

@@ -37,23 +37,51 @@ inline uint64_t load_be64(const unsigned char* p) {
   return __builtin_bswap64(v);
 }
 
+// Fully unrolled rounds over a rolling 16-word message schedule; the eight
+// working variables rotate by renaming (no moves), so each round is the
+// FIPS 180-4 arithmetic and nothing else.
+#define NWK_S0(x) (rotr(x, 28) ^ rotr(x, 34) ^ rotr(x, 39))
+#define NWK_S1(x) (rotr(x, 14) ^ rotr(x, 18) ^ rotr(x, 41))
+#define NWK_s0(x) (rotr(x, 1) ^ rotr(x, 8) ^ ((x) >> 7))
+#define NWK_s1(x) (rotr(x, 19) ^ rotr(x, 61) ^ ((x) >> 6))
+#define NWK_ROUND(a, b, c, d, e, f, g, h, t, wt)                                   \
+  do {                                                                          \
+    const uint64_t t1 = h + NWK_S1(e) + (g ^ (e & (f ^ g))) + kK[t] + (wt);      \
+    const uint64_t t2 = NWK_S0(a) + ((a & b) | (c & (a | b)));                  \
+    d += t1;                                                                    \
+    h = t1 + t2;                                                                \
+  } while (0)
+
 void compress(uint64_t st[8], const unsigned char* blk) {
-  uint64_t w[80];
+  uint64_t w[16];
   for (int t = 0; t < 16; ++t) w[t] = load_be64(blk + 8 * t);
-  for (int t = 16; t < 80; ++t) {
-    const uint64_t s0 = rotr(w[t - 15], 1) ^ rotr(w[t - 15], 8) ^ (w[t - 15] >> 7);
-    const uint64_t s1 = rotr(w[t - 2], 19) ^ rotr(w[t - 2], 61) ^ (w[t - 2] >> 6);
-    w[t] = w[t - 16] + s0 + w[t - 7] + s1;
-  }
   uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-  for (int t = 0; t < 80; ++t) {
-    const uint64_t t1 = h + (rotr(e, 14) ^ rotr(e, 18) ^ rotr(e, 41)) + ((e & f) ^ (~e & g)) + kK[t] + w[t];
-    const uint64_t t2 = (rotr(a, 28) ^ rotr(a, 34) ^ rotr(a, 39)) + ((a & b) ^ (a & c) ^ (b & c));
-    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+#pragma unroll
+  for (int t = 0; t < 80; t += 8) {
+    if (t >= 16) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int u = t + q;
+        w[u & 15] += NWK_s1(w[(u - 2) & 15]) + w[(u - 7) & 15] + NWK_s0(w[(u - 15) & 15]);
+      }
+    }
+    NWK_ROUND(a, b, c, d, e, f, g, h, t + 0, w[(t + 0) & 15]);
+    NWK_ROUND(h, a, b, c, d, e, f, g, t + 1, w[(t + 1) & 15]);
+    NWK_ROUND(g, h, a, b, c, d, e, f, t + 2, w[(t + 2) & 15]);
+    NWK_ROUND(f, g, h, a, b, c, d, e, t + 3, w[(t + 3) & 15]);
+    NWK_ROUND(e, f, g, h, a, b, c, d, t + 4, w[(t + 4) & 15]);
+    NWK_ROUND(d, e, f, g, h, a, b, c, t + 5, w[(t + 5) & 15]);
+    NWK_ROUND(c, d, e, f, g, h, a, b, t + 6, w[(t + 6) & 15]);
+    NWK_ROUND(b, c, d, e, f, g, h, a, t + 7, w[(t + 7) & 15]);
   }
   st[0] += a; st[1] += b; st[2] += c; st[3] += d;
   st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
+#undef NWK_ROUND
+#undef NWK_S0
+#undef NWK_S1
+#undef NWK_s0
+#undef NWK_s1
 
 }  // namespace
 

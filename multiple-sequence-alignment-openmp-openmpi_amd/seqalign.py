@@ -61,6 +61,8 @@ SIGNATURES = {
     "nwk_get_minimum_penalties": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P, _P, _P]),
     "nwk_get_minimum_penalty": (ctypes.c_int, [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _P, _P]),
     "nwk_align_pairs_affine": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _I32, _P, _P]),
+    "nwk_align_all": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P]),
+    "nwk_align_all_affine": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),
     "nwk_get_minimum_penalty_affine": (ctypes.c_int, [_P, _P, _I32, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),
     "nwk_get_minimum_penalties_affine": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P]),
     "nwk_shard_pairs": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
@@ -177,6 +179,20 @@ class Engine:
         hs = np.zeros((max(n, 1), 64), dtype=np.uint8)
         _check(self.lib.nwk_align_pairs(self._ctx, _ptr(ids), n, pxy, pgap, _ptr(pen), _ptr(hs)))
         return pen[:n], hs[:n]
+
+    def align_all(self, pxy, pgap, affine=None):
+        """All pairs of the current set + the chained answer hash (getMinimumPenalties
+        on this context): returns (hash, penalties int32[P], raw hashes uint8[P,64]).
+        affine=(go, ge) selects the affine-gap variant."""
+        P = self.k * (self.k - 1) // 2
+        pen = np.zeros(max(P, 1), dtype=np.int32)
+        hs = np.zeros((max(P, 1), 64), dtype=np.uint8)
+        out = ctypes.create_string_buffer(129)
+        if affine:
+            _check(self.lib.nwk_align_all_affine(self._ctx, pxy, affine[0], affine[1], _ptr(pen), _ptr(hs), out))
+        else:
+            _check(self.lib.nwk_align_all(self._ctx, pxy, pgap, _ptr(pen), _ptr(hs), out))
+        return out.value.decode(), pen[:P], hs[:P]
 
     def align_pairs_affine(self, pair_ids, pxy, go, ge):
         """Affine-gap variant of align_pairs."""

@@ -239,3 +239,27 @@ def test_affine_multi_batch_and_api(golden):
     assert seqalign.getMinimumPenaltiesAffine(genes, len(genes), 3, 4, 1, pens) == h and pens == opens
     with pytest.raises(seqalign.NwkError):
         seqalign.getMinimumPenaltiesAffine(genes, len(genes), -1, 4, 1, pens)
+
+
+@pytest.mark.parametrize("name", ["mseq1", "xulin_test", "big13", "k1", "k0", "k2_same"])
+def test_align_all_pipelined_chain(engine, golden, name):
+    """nwk_align_all: the chain runs while batches are in flight; same answer."""
+    c = golden[name]
+    pxy, pgap, genes = case_input(c)
+    engine.set_sequences(genes)
+    h, pen, hs = engine.align_all(pxy, pgap)
+    assert h == c["hash"] and [int(v) for v in pen] == c["penalties"]
+
+
+def test_align_all_multi_batch_affine():
+    r = random.Random(33)
+    genes = _rand_genes(r, 8, 500, 1200, ACGT)
+    with seqalign.Engine(device=0, workspace_bytes=3 << 20) as e:
+        e.set_sequences(genes)
+        h, pen, hs = e.align_all(3, 2)
+        assert e.stats()["batches"] > 2
+        ha, pena, _ = e.align_all(3, None, affine=(4, 1))
+    oh, opens, _ = oracle.all_pairs(genes, 3, 2)
+    assert h == oh and [int(v) for v in pen] == opens
+    ah, apens, _ = oracle.all_pairs_affine(genes, 3, 4, 1)
+    assert ha == ah and [int(v) for v in pena] == apens
