@@ -8,11 +8,12 @@ namespace nwk {
 constexpr int kWave = 64;
 constexpr int kRows = 8;                  // DP rows per lane (R)
 constexpr int kBandRows = kWave * kRows;  // rows per band = one wave's task
-constexpr int kEPad = 64;                 // E entries before column 0
+constexpr int kEPad = 128;                // E / SEL entries before column 0
+constexpr int kETail = 384;               // E / SEL entries past the last column
 // Sequence-code buffer padding.  The traceback stages 256-byte windows by
 // LDS-DMA: y windows start up to 96 bytes before a sequence, x windows end up
 // to ~660 bytes past the last 512-row band's first row.
-constexpr int kCodesFrontPad = 128;
+constexpr int kCodesFrontPad = 256;
 constexpr int kCodesTailPad = 1024;
 
 // Recurrence variants (see DESIGN.md "Kernels").
@@ -21,6 +22,7 @@ enum Mode : int {
   kCompare = 1,  // any bytes, penalties >= 0: byte compare + select
   kLiteral = 2,  // any penalties: skel:215-224 literally (match ? diag : min3)
   kAffine = 3,   // affine gaps: 4-bit traceback codes, compare mode
+  kPacked = 4,   // kProfile at W = 4 with two cells per register (int16 pairs), packed layout
 };
 
 // One pair of the batch.  All offsets are element offsets into the
@@ -35,7 +37,7 @@ struct PairDesc {
   int32_t m, n;
   int32_t nbands;   // ceil(m / kBandRows)
   int32_t nchunks;  // ceil(n / 64): 64-column boundary chunks
-  int32_t sblocks;  // 64-step super-blocks per band = nchunks + 1
+  int32_t sblocks;  // 64-step super-blocks per band = nchunks + 1 (kPacked: + 2)
   int32_t slot;     // index of this pair in the batch's result arrays
 };
 
@@ -45,6 +47,7 @@ struct FillArgs {
   int ntasks;
   const uint8_t* codes;    // sequence codes (x rows, y columns)
   const uint32_t* E;       // expanded column codes, 4 per dword
+  const uint32_t* sel;     // kPacked: per column v_perm selector {y[a], hi, 4+y[a-1], hi}
   uint32_t* mat;           // packed G = H - (i+j)*pgap, W bits per cell
   unsigned long long* bnd; // {epoch:32 | G:32} granules, one per boundary cell
   unsigned* counter;       // task dequeue head

@@ -199,43 +199,74 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const lds_u32*)p;
 }
 
-template <int W>
-struct TbConf {
-  static constexpr int SPD = 32 / W;
-  static constexpr int TC = 8;                      // dword columns per window
-  static constexpr int TS = TC * SPD;               // steps per window
-  static constexpr int OV = (11 + SPD - 1) / SPD;   // columns below: a block reaches s-10
-  static constexpr int CC = TC + OV;
-  static constexpr int TL = 16;                     // lanes (8-row groups) per tile
-  static constexpr int TILE = CC * kRows * TL;      // dwords
-  static constexpr int NB = 1;                       // single buffer: LDS per block bounds fill occupancy
-  static constexpr int YLO = 96;                    // y window starts 96 columns below the window
-  static_assert(TILE % 64 == 0, "tile = whole DMA instructions");
-  static_assert(TS + YLO <= 256, "y window must fit one DMA");
-  static_assert(YLO <= kCodesFrontPad, "y windows must stay inside the codes buffer");
+// Stored-matrix layouts.
+//  plain  (nw_align, W bits):  per band, dword (c*8 + r)*64 + t holds row r of
+//         lane t for steps [c*SPD, (c+1)*SPD), SPD = 32/W; cell (row 8t+r,
+//         column j) is step s = j-1+t, bits W*(s%SPD).
+//  packed (nw_align_pk, W = 4): dword (g*4 + q)*64 + t holds rows q and q+4
+//         of lane t for steps [4g, 4g+4); cell (8t+r, j) is step
+//         s = j-1+2t+h (h = r>>2: rows 4..7 run one column behind rows 0..3),
+//         nibble at bit 8*(2*(s&1)+h) + 4*((s>>1)&1).
+template <int W, bool PK>
+struct Lay {
+  static constexpr int SPC = 32 / W;  // steps per column unit
+  static constexpr int RPC = kRows;   // dwords per column unit per lane
+  __device__ static int step(int t, int r, int j) { (void)r; return j - 1 + t; }
+  __device__ static int slot(int r) { return r; }
+  __device__ static int shift(int s, int r) { (void)r; return W == 32 ? 0 : W * (s & (SPC - 1)); }
+};
+template <>
+struct Lay<4, true> {
+  static constexpr int SPC = 4;
+  static constexpr int RPC = 4;
+  __device__ static int step(int t, int r, int j) { return j - 1 + 2 * t + (r >> 2); }
+  __device__ static int slot(int r) { return r & 3; }
+  __device__ static int shift(int s, int r) { return 8 * (2 * (s & 1) + (r >> 2)) + 4 * ((s >> 1) & 1); }
 };
 
-template <int W>
+template <int W, bool PK = false>
+struct TbConf {
+  using L = Lay<W, PK>;
+  static constexpr int SPC = L::SPC;
+  static constexpr int TC = PK ? 16 : 8;            // column units per window
+  static constexpr int TS = TC * SPC;               // steps per window
+  // column units below the window: a block reaches 10 (plain) / 12 (packed) steps below its cell
+  static constexpr int OV = PK ? 4 : (11 + SPC - 1) / SPC;
+  static constexpr int CC = TC + OV;
+  static constexpr int TL = 16;                     // lanes (8-row groups) per tile
+  static constexpr int TILE = CC * L::RPC * TL;     // dwords
+  static constexpr int NB = 1;                       // single buffer: LDS per block bounds fill occupancy
+  static constexpr int YLO = 96;                    // plain: y window starts 96 columns below the window
+  static_assert(TILE % 64 == 0, "tile = whole DMA instructions");
+  static_assert(L::RPC % 4 == 0, "a DMA covers 4 dword rows x 16 lanes");
+  static_assert(PK || TS + YLO <= 256, "y window must fit one DMA");
+  static_assert(PK ? (TS + 56 <= 256 && 2 * 63 + 48 + 3 <= kCodesFrontPad) : YLO <= kCodesFrontPad,
+                "y windows must stay inside the codes buffer");
+  // first y column (0-based) of the 256-byte window staged for step window q, lanes [t0, t0+16)
+  __device__ static int ywin(int q, int t0) { return PK ? ((TS * q - 2 * t0 - 48) & ~3) : TS * q - YLO; }
+};
+
+template <int W, bool PK = false>
 struct TbLds {
-  unsigned tile[TbConf<W>::NB][TbConf<W>::TILE];
-  unsigned xs[TbConf<W>::NB][64];
-  unsigned ys[TbConf<W>::NB][64];
+  unsigned tile[TbConf<W, PK>::NB][TbConf<W, PK>::TILE];
+  unsigned xs[TbConf<W, PK>::NB][64];
+  unsigned ys[TbConf<W, PK>::NB][64];
   unsigned obuf[64];   // 256-byte ring of traceback moves, flushed to HBM in dwords
 };
 
-template <int W>
+template <int W, bool PK = false>
 __device__ __forceinline__ unsigned getG_global(const unsigned* M, const PairDesc& pd, int64_t bdw, int i, int j) {
   if (i == 0 || j == 0) return 0u;
-  constexpr int SPD = 32 / W;
+  using L = Lay<W, PK>;
   const int w = i - 1;
   const int b = w / kBandRows;
   const int wr = w - b * kBandRows;
   const int t = wr / kRows;
   const int r = wr - t * kRows;
-  const int s = j - 1 + t;
-  const unsigned d = M[pd.mat_off + (int64_t)b * bdw + ((int64_t)(s / SPD) * kRows + r) * kWave + t];
+  const int s = L::step(t, r, j);
+  const unsigned d = M[pd.mat_off + (int64_t)b * bdw + ((int64_t)(s / L::SPC) * L::RPC + L::slot(r)) * kWave + t];
   if constexpr (W == 32) return d;
-  else return (d >> (W * (s % SPD))) & ((1u << W) - 1u);
+  else return (d >> L::shift(s, r)) & ((1u << W) - 1u);
 }
 
 struct Five { unsigned v[5]; };
@@ -243,27 +274,28 @@ struct Five { unsigned v[5]; };
 // Rare cells (band above, outside the staged window) come from global memory
 // in a non-inlined call, so the wait for those loads -- which also drains the
 // tile prefetch -- stays on this path.
-template <int W>
+template <int W, bool PK>
 __device__ __noinline__ Five tb_fallback(const unsigned* mat, const PairDesc& pd, int64_t bdw, const uint8_t* xg,
                                          const uint8_t* yg, int ci, int cj, bool fx, bool fy, bool fg, bool fu,
                                          bool fd, int shg, int shu, int shd, Five in) {
   Five o = in;
   if (fx) o.v[0] = xg[ci - 1];
   if (fy) o.v[1] = yg[cj - 1];
-  if (fg) o.v[2] = getG_global<W>(mat, pd, bdw, ci, cj) << shg;
-  if (fu) o.v[3] = getG_global<W>(mat, pd, bdw, ci - 1, cj) << shu;
-  if (fd) o.v[4] = getG_global<W>(mat, pd, bdw, ci - 1, cj - 1) << shd;
+  if (fg) o.v[2] = getG_global<W, PK>(mat, pd, bdw, ci, cj) << shg;
+  if (fu) o.v[3] = getG_global<W, PK>(mat, pd, bdw, ci - 1, cj) << shu;
+  if (fd) o.v[4] = getG_global<W, PK>(mat, pd, bdw, ci - 1, cj - 1) << shd;
   return o;
 }
 
-template <int W>
-__device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd, TbLds<W>& L, int lane) {
-  using C = TbConf<W>;
-  constexpr int SPD = C::SPD;
-  constexpr int LSPD = SPD == 8 ? 3 : SPD == 4 ? 2 : SPD == 2 ? 1 : 0;
+template <int W, bool PK = false>
+__device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd, TbLds<W, PK>& L, int lane) {
+  using C = TbConf<W, PK>;
+  using Y = Lay<W, PK>;
+  constexpr int SPC = Y::SPC;
+  constexpr int RPC = Y::RPC;
   constexpr unsigned MASK = W == 32 ? 0xffffffffu : ((1u << (W & 31)) - 1u);
   const int64_t bdw = band_dwords(W, pd.sblocks);
-  const int ncols = 64 * pd.sblocks / SPD;
+  const int ncols = 64 * pd.sblocks / SPC;
   const uint8_t* xg = a.codes + pd.x_off;
   const uint8_t* yg = a.codes + pd.y_off;
   const unsigned* mb = a.mat + pd.mat_off;
@@ -271,22 +303,23 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
   unsigned long long cy_sw = 0, cy_blk = 0, n_blk = 0, n_sw = 0, n_sync = 0, tA = 0, tB;
 
   // Stage tile (b, q, t0) into buffer buf by LDS-DMA: lanes [t0, t0+16) of
-  // band b, dword columns [TC*q - OV, TC*q + TC) (clamped), the x codes of
-  // rows [512b + 8t0, +256) and the y codes of columns [TS*q - YLO, +256).
-  // DMA k covers column k/2, rows 4(k&1) + lane/16, lanes t0 + lane%16.
+  // band b, column units [TC*q - OV, TC*q + TC) (clamped), the x codes of
+  // rows [512b + 8t0, +256) and the y codes of columns [ywin(q, t0), +256).
+  // DMA k covers column unit k/(RPC/4), dword rows 4(k%(RPC/4)) + lane/16,
+  // lanes t0 + lane%16.
   const int lane_off = (lane >> 4) * kWave + (lane & 15);
   auto issue = [&](int buf, int b, int q, int t0) {
     const unsigned* src = mb + (int64_t)b * bdw + t0 + lane_off;
 #pragma unroll
     for (int k = 0; k < C::TILE / 64; ++k) {
-      int c = C::TC * q - C::OV + (k >> 1);
+      int c = C::TC * q - C::OV + k / (RPC / 4);
       c = c < 0 ? 0 : (c >= ncols ? ncols - 1 : c);
-      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (int64_t)c * (kRows * kWave) + (k & 1) * 4 * kWave),
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (int64_t)c * (RPC * kWave) + 4 * (k % (RPC / 4)) * kWave),
                                        (lds_void*)&L.tile[buf][64 * k], 4, 0, 0);
     }
     const unsigned* xsrc = reinterpret_cast<const unsigned*>(xg + (int64_t)b * kBandRows + 8 * t0);
     __builtin_amdgcn_global_load_lds((gbl_void*)(xsrc + lane), (lds_void*)&L.xs[buf][0], 4, 0, 0);
-    const unsigned* ysrc = reinterpret_cast<const unsigned*>(yg + (int64_t)C::TS * q - C::YLO);
+    const unsigned* ysrc = reinterpret_cast<const unsigned*>(yg + C::ywin(q, t0));
     __builtin_amdgcn_global_load_lds((gbl_void*)(ysrc + lane), (lds_void*)&L.ys[buf][0], 4, 0, 0);
   };
   // The walk reads LDS only through inline asm, so the compiler does not
@@ -295,7 +328,7 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
 
   uint8_t* ops = a.ops + pd.ops_off;
   int i = pd.m, j = pd.n, Lc = 0, flushed = 0;
-  int tb = -1, tq = 0, tt0 = 0, cur = 0, pb = -1, pq = 0, pt0 = 0;
+  int tb = -1, tq = 0, tt0 = 0, cur = 0, pb = -1, pq = 0, pt0 = 0, yw = 0;
   const unsigned ob = lds_addr(&L.obuf[0]);
   // Moves go to an LDS ring (ds_write_b8, no VMEM) and reach HBM as whole
   // dwords: a store in flight would otherwise make every drain() wait for it.
@@ -317,7 +350,7 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
     {  // ---- make the tile holding the 8x8 block at (i, j) current
       const int b = (i - 1) / kBandRows;
       const int tl = t > 0 ? t - 1 : 0;  // lowest lane of this band the block touches
-      const int s = j - 1 + t;
+      const int s = Y::step(t, w & 7, j);
       if (b != tb || s < C::TS * tq || tl < tt0 || t >= tt0 + C::TL) {
         const int q = s / C::TS;
         drain();
@@ -337,6 +370,7 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
         }
         tb = b;
         tq = q;
+        yw = C::ywin(q, tt0);
         pb = -1;
         if (C::NB == 2 && q > 0) {  // the walk moves down the band: prefetch the next window
           pt0 = max(0, t - (C::TL - 1));
@@ -351,6 +385,12 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
     const int cbase = C::TC * tq - C::OV;
     const unsigned tbase = lds_addr(&L.tile[cur][0]);
     const unsigned xb = lds_addr(&L.xs[cur][0]), yb = lds_addr(&L.ys[cur][0]);
+    // LDS address of staged cell (row ww of band tb, column jj) and its bit shift
+    auto taddr = [&](int ww, int jj, int& sh) -> unsigned {
+      const int tt = ww >> 3, rr = ww & 7, ss = Y::step(tt, rr, jj);
+      sh = Y::shift(ss, rr);
+      return tbase + 4u * (unsigned)(((ss / SPC - cbase) * RPC + Y::slot(rr)) * C::TL + (tt - tt0));
+    };
     unsigned vx, vy, vg, vu, vd;
     int shg, shu, shd;
     bool bg, bu, bd;  // border cells (G = 0)
@@ -358,17 +398,12 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
     // this band, inside the staged window and off the border -> branch-free.
     if (w >= 8 && j >= 9) {
       const int wc = w - li, wu = wc - 1;
-      const int tc = wc >> 3, rc = wc & 7, tu = wu >> 3, ru = wu & 7;
-      const int jc = j - 1 - lj;  // 0-based column of the cell
-      const int sc = jc + tc, su = jc + tu, sd = su - 1;
-      const unsigned ag = tbase + 4u * (unsigned)((((sc >> LSPD) - cbase) * kRows + rc) * C::TL + tc - tt0);
-      const unsigned au = tbase + 4u * (unsigned)((((su >> LSPD) - cbase) * kRows + ru) * C::TL + tu - tt0);
-      const unsigned ad = tbase + 4u * (unsigned)((((sd >> LSPD) - cbase) * kRows + ru) * C::TL + tu - tt0);
-      shg = W == 32 ? 0 : W * (sc & (SPD - 1));
-      shu = W == 32 ? 0 : W * (su & (SPD - 1));
-      shd = W == 32 ? 0 : W * (sd & (SPD - 1));
+      const int jc = j - lj;  // 1-based column of the cell
+      const unsigned ag = taddr(wc, jc, shg);
+      const unsigned au = taddr(wu, jc, shu);
+      const unsigned ad = taddr(wu, jc - 1, shd);
       const unsigned ax = xb + (unsigned)(wc - 8 * tt0);
-      const unsigned ay = yb + (unsigned)(jc - (C::TS * tq - C::YLO));
+      const unsigned ay = yb + (unsigned)(jc - 1 - yw);
       asm volatile(
           "ds_read_u8 %0, %5\n\t"
           "ds_read_u8 %1, %6\n\t"
@@ -382,18 +417,18 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
       bg = bu = bd = false;
     } else {  // slow path: band top, border, or outside the window
       const int ci = i - li, cj = j - lj;
-      const int slo = C::TS * tq - C::OV * SPD, shi = C::TS * tq + C::TS;
+      const int slo = C::TS * tq - C::OV * SPC, shi = C::TS * tq + C::TS;
       // LDS address of G(ii, jj), ~0u on the border (G = 0), ~1u if not staged
       auto gaddr = [&](int ii, int jj, int& sh) -> unsigned {
         if (ii <= 0 || jj <= 0) { sh = 0; return ~0u; }
         const int ww = ii - 1 - tb * kBandRows;
-        const int tt = ww >> 3, rr = ww & 7, ss = jj - 1 + tt;
-        sh = W == 32 ? 0 : W * (ss & (SPD - 1));
+        const int tt = ww >> 3, rr = ww & 7, ss = Y::step(tt, rr, jj);
+        sh = Y::shift(ss, rr);
         if (ww < 0 || tt < tt0 || tt >= tt0 + C::TL || ss < slo || ss >= shi) return ~1u;
-        return tbase + 4u * (unsigned)(((ss / SPD - cbase) * kRows + rr) * C::TL + (tt - tt0));
+        return taddr(ww, jj, sh);
       };
       const unsigned ag = gaddr(ci, cj, shg), au = gaddr(ci - 1, cj, shu), ad = gaddr(ci - 1, cj - 1, shd);
-      const int wx = ci - 1 - (tb * kBandRows + 8 * tt0), wy = cj - 1 - (C::TS * tq - C::YLO);
+      const int wx = ci - 1 - (tb * kBandRows + 8 * tt0), wy = cj - 1 - yw;
       const bool xin = ci >= 1 && wx >= 0 && wx < 256, yin = cj >= 1 && wy >= 0 && wy < 256;
       const unsigned ax = xin ? xb + (unsigned)wx : xb;
       const unsigned ay = yin ? yb + (unsigned)wy : yb;
@@ -409,8 +444,8 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
           : "memory");
       const bool fx = !xin && ci >= 1, fy = !yin && cj >= 1;
       if (fx || fy || ag == ~1u || au == ~1u || ad == ~1u) {
-        const Five f = tb_fallback<W>(a.mat, pd, bdw, xg, yg, ci, cj, fx, fy, ag == ~1u, au == ~1u, ad == ~1u, shg,
-                                      shu, shd, Five{vx, vy, vg, vu, vd});
+        const Five f = tb_fallback<W, PK>(a.mat, pd, bdw, xg, yg, ci, cj, fx, fy, ag == ~1u, au == ~1u, ad == ~1u,
+                                          shg, shu, shd, Five{vx, vy, vg, vu, vd});
         vx = f.v[0]; vy = f.v[1]; vg = f.v[2]; vu = f.v[3]; vd = f.v[4];
       }
       bg = ag == ~0u;
@@ -603,6 +638,229 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
 
 
 // ===========================================================================
+// Packed fill (kPacked): the kProfile recurrence at W = 4 with two cells per
+// VGPR as int16 pairs.  On gfx950 v_pk_min_i16 / v_pk_add_u16 / v_perm_b32
+// issue at the rate of ONE v_min3 / v_bfe / v_alignbit (profiles/r01/
+// valu_probe_gfx950.txt), so per cell the substitution lookup (v_bfe -> half
+// a v_perm), the add and the 4-bit packing (v_alignbit -> a quarter v_perm +
+// v_bfi) all halve; the two mins stay one instruction-equivalent.
+//
+// Lane t holds 8 rows as 4 packed registers P[q] = {row q at column
+// s-2t+1, row q+4 at column s-2t} (rows 4..7 run one column behind rows 0..3,
+// so row q+4 reads row q+3 of the previous step: no same-step dependence
+// between halves; lanes are skewed by 2 columns).  Values are G relative to a
+// wave-uniform base (a multiple of 16, so G mod 16 is unchanged), re-centred
+// every super-block: across one wave G spans < 1400*pgap + 128*pgap, inside
+// int16 for the W = 4 range pgap <= 7.  Per cell, with K from the row pair's
+// profile bytes selected by the column's SEL word (sign-extended by the 'hi'
+// selector byte: both K < 0, or both >= 0):
+//     P[q] = pk_min(pk_min(diag + K, left), up)
+// Storage (packed layout, see Lay<4, true>): per 4 steps and q, one dword:
+// v_perm gathers the low bytes of two steps' P[q] and v_bfi merges two such
+// words as nibbles.
+// ===========================================================================
+typedef short __attribute__((ext_vector_type(2))) s16x2;
+__device__ __forceinline__ unsigned pk_min(unsigned a, unsigned b) {
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_min(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b)));
+}
+__device__ __forceinline__ unsigned pk_add(unsigned a, unsigned b) {
+  return __builtin_bit_cast(unsigned, __builtin_bit_cast(s16x2, a) + __builtin_bit_cast(s16x2, b));
+}
+__device__ __forceinline__ unsigned pk_sub(unsigned a, unsigned b) {
+  return __builtin_bit_cast(unsigned, __builtin_bit_cast(s16x2, a) - __builtin_bit_cast(s16x2, b));
+}
+__device__ __forceinline__ void asm_load_S3(const unsigned* p, unsigned& a, unsigned& b, unsigned& c) {
+  asm volatile(
+      "global_load_dword %0, %3, off\n\tglobal_load_dword %1, %3, off offset:256\n\t"
+      "global_load_dword %2, %3, off offset:512"
+      : "=&v"(a), "=&v"(b), "=&v"(c)
+      : "v"(p)
+      : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_keep3(unsigned& a, unsigned& b, unsigned& c, u64& d) {
+  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N) : "memory");
+}
+
+// Eight wavefront steps s0..s0+7 (s0 % 8 == 0).
+//   bslot: LDS ring of (B[s0+1 .. s0+8] - base) << 16 (band-above row)
+//   srow:  LDS SEL window at this lane's column for step s0 (8 words)
+//   pub:   publish the stage window after the stage shift of step 7
+template <bool MASK>
+__device__ __forceinline__ void step_block_pk(int s0, int lane, unsigned (&P)[4], unsigned& U, unsigned& stage,
+                                              const unsigned (&pl)[4], const unsigned (&ph)[4], const unsigned* srow,
+                                              const int* bslot, unsigned* mptr, bool pub, u64* gpub, unsigned epoch,
+                                              int base) {
+  const int4 bA = *reinterpret_cast<const int4*>(bslot);
+  const int4 bB = *reinterpret_cast<const int4*>(bslot + 4);
+  const int bv[8] = {bA.x, bA.y, bA.z, bA.w, bB.x, bB.y, bB.z, bB.w};
+  const uint2* sp = reinterpret_cast<const uint2*>(srow);
+  const uint2 c0 = sp[0], c1 = sp[1], c2 = sp[2], c3 = sp[3];
+  const unsigned sel[8] = {c0.x, c0.y, c1.x, c1.y, c2.x, c2.y, c3.x, c3.y};
+  unsigned Xa[4];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    // lane 63's {row 3, row 7} of the previous step enters the publish window
+    stage = (unsigned)__builtin_amdgcn_update_dpp((int)P[3], (int)stage, 0x130 /*wave_shl:1*/, 0xf, 0xf, false);
+    if (k == 7 && pub) st_granule(gpub, epoch, ((int)stage >> 16) + base);
+    // up of the first row pair: {lane t-1's row 7 (lane 0: band above), own row 3}, previous step
+    const unsigned x = (unsigned)__builtin_amdgcn_update_dpp(bv[k], (int)P[3], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
+    const unsigned up = __builtin_amdgcn_alignbit(P[3], x, 16);
+    const unsigned dg0 = U;
+    U = up;
+    unsigned sk = sel[k];
+    asm volatile("" : "+v"(sk));
+    unsigned Pn[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned K = __builtin_amdgcn_perm(ph[q], pl[q], sk);
+      const unsigned dg = q ? P[q - 1] : dg0;
+      const unsigned uq = q ? Pn[q - 1] : up;
+      Pn[q] = pk_min(pk_min(pk_add(dg, K), P[q]), uq);
+    }
+    if constexpr (MASK) {  // columns <= 0 stay on the border (G = 0; base is 0 here)
+      const int s = s0 + k;
+      const unsigned M = s > 2 * lane ? 0xffffffffu : (s == 2 * lane ? 0x0000ffffu : 0u);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Pn[q] &= M;
+    }
+    if (k & 1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        // {row q, row q+4} x {step k-1, step k}: low bytes (nibble + 4 junk bits)
+        const unsigned X = __builtin_amdgcn_perm(Pn[q], P[q], 0x06040200u);
+        if ((k & 3) == 1) {
+          Xa[q] = X;
+        } else {
+          const unsigned D = (Xa[q] & 0x0f0f0f0fu) | ((X << 4) & 0xf0f0f0f0u);
+          __builtin_nontemporal_store(D, mptr + ((k >> 2) * 4 + q) * kWave);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) P[q] = Pn[q];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__global__ __launch_bounds__(256) void nw_align_pk(FillArgs a) {
+  constexpr int W = 4;
+  __shared__ __attribute__((aligned(16))) int ring_all[4][128];
+  // SEL window per super-block: SEL[64sb-128 .. 64sb+64), two slots per wave
+  __shared__ __attribute__((aligned(16))) unsigned swin_all[4][384];
+  __shared__ __attribute__((aligned(16))) TbLds<W, true> tbl[4];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  int* ring = ring_all[wid];
+  unsigned* swin = swin_all[wid];
+
+  for (;;) {
+    unsigned tk = 0;
+    if (lane == 0) tk = atomicAdd(a.counter, 1u);
+    tk = __builtin_amdgcn_readfirstlane(tk);
+    if (tk >= (unsigned)a.ntasks) return;
+    if (__hip_atomic_load((gu32*)a.err, RLX_AGENT) != 0u) return;
+    const int2 task = a.tasks[tk];
+    const PairDesc pd = a.pairs[task.x];
+    const int band = task.y;
+    const int row0 = band * kBandRows + lane * kRows;
+    unsigned xq[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      const int row = row0 + r;
+      const unsigned cc = row < pd.m ? a.codes[pd.x_off + row] : 0u;
+      unsigned p = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) p |= ((unsigned)(cc == (unsigned)q ? a.K0 : a.K1) & 0xffu) << (8 * q);
+      xq[r] = p;
+    }
+    const unsigned pl[4] = {xq[0], xq[1], xq[2], xq[3]};
+    const unsigned ph[4] = {xq[4], xq[5], xq[6], xq[7]};
+
+    const bool from_above = band > 0;
+    const bool to_below = band + 1 < pd.nbands;
+    const int64_t bstride = (int64_t)pd.nchunks * 64;
+    const u64* gin = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)(band > 0 ? band - 1 : 0) * bstride + lane;
+    const int last_chunk = pd.nchunks > 0 ? pd.nchunks - 1 : 0;
+    u64* gout = a.bnd + pd.bnd_off + (int64_t)band * bstride + lane;
+    unsigned* mptr = a.mat + pd.mat_off + (int64_t)band * band_dwords(W, pd.sblocks) + lane;
+
+    unsigned P[4] = {0u, 0u, 0u, 0u};
+    unsigned U = 0, stage = 0;
+    int base = 0;
+    u64 pend = 0;
+    const unsigned* Sg = a.sel + pd.e_off - 128 + lane;
+    unsigned sw0, sw1, sw2;
+    asm_load_S3(Sg, sw0, sw1, sw2);
+    asm_load_granule(gin, pend);
+    wait_vm_keep3<0>(sw0, sw1, sw2, pend);
+    bool ok = true;
+    constexpr int kBlockStores = 8;
+
+    for (int sb = 0; sb < pd.sblocks; ++sb) {
+      // --- band-above row for this super-block: B[64sb+1 .. 64sb+64] = chunk sb
+      int bval = 0;
+      if (from_above && sb < pd.nchunks) {
+        if (!__all((unsigned)(pend >> 32) == a.epoch)) {
+          pend = wait_granules(gin + 64 * sb, a.epoch, pend, a.err);
+          if (!__all((unsigned)(pend >> 32) == a.epoch)) { ok = false; break; }
+        }
+        bval = (int)(unsigned)pend;
+      }
+      asm_load_granule(gin + 64 * min(sb + 1, last_chunk), pend);
+      // --- re-centre the base (after the masked super-blocks 0 and 1)
+      if (sb >= 2) {
+        const int ref = (int)(short)(__builtin_amdgcn_readlane((int)P[0], 32) & 0xffff);
+        const int delta = ref & ~15;
+        const unsigned dd = ((unsigned)delta & 0xffffu) * 0x10001u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) P[q] = pk_sub(P[q], dd);
+        U = pk_sub(U, dd);
+        stage -= (unsigned)delta << 16;
+        base += delta;
+      }
+      int* slot = ring + (sb & 1) * 64;
+      slot[lane] = (int)((unsigned)(bval - base) << 16);
+      unsigned* w = swin + (sb & 1) * 192;
+      w[lane] = sw0;
+      w[64 + lane] = sw1;
+      w[128 + lane] = sw2;
+      asm_load_S3(Sg + 64 * (sb + 1), sw0, sw1, sw2);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+
+      const bool pub_sb = to_below && sb >= 2 && sb - 2 < pd.nchunks;
+      u64* gpub = gout + 64 * (sb >= 2 ? sb - 2 : 0);
+      for (int blk = 0; blk < 8; ++blk) {
+        const int s0 = sb * 64 + blk * 8;
+        const unsigned* srow = w + blk * 8 + 128 - 2 * lane;
+        const bool pub = pub_sb && blk == 7;
+        if (sb < 2)
+          step_block_pk<true>(s0, lane, P, U, stage, pl, ph, srow, slot + blk * 8, mptr, pub, gpub, a.epoch, base);
+        else
+          step_block_pk<false>(s0, lane, P, U, stage, pl, ph, srow, slot + blk * 8, mptr, pub, gpub, a.epoch, base);
+        mptr += 2 * 4 * kWave;
+        wait_vm_keep3<kBlockStores>(sw0, sw1, sw2, pend);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (!ok) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add((gu32*)(a.done + pd.slot), 1u, RLX_AGENT);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev + 1u == (unsigned)pd.nbands) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      trace_pair<W, true>(a, pd, tbl[wid], lane);
+    }
+  }
+}
+
+// ===========================================================================
 // Affine-gap variant (build-defined, see oracle
 // nwo_pair_affine):
 //   E = min(E[i][j-1] + ge, H[i][j-1] + go + ge)      F = min(F[i-1][j] + ge, H[i-1][j] + go + ge)
@@ -690,7 +948,7 @@ __device__ __forceinline__ void wait_vm_keep4(unsigned& a, unsigned& b, u64& c, 
 // charges go + ge there, ge for the others).
 __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairDesc& pd, TbLds<4>& L, int lane, unsigned* prog) {
   using C = TbConf<4>;
-  constexpr int SPD = C::SPD;
+  constexpr int SPD = C::SPC;
   const int64_t bdw = band_dwords(4, pd.sblocks);
   const int ncols = 64 * pd.sblocks / SPD;
   const unsigned* mb = a.mat + pd.mat_off;
@@ -755,7 +1013,7 @@ __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairD
         asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ad) : "memory");
         code = (v >> (4 * (ss & (SPD - 1)))) & 15u;
       } else {
-        code = getG_global<4>(a.mat, pd, bdw, ci, cj);
+        code = getG_global<4, false>(a.mat, pd, bdw, ci, cj);
       }
     }
     if (prog && lane == 0) __hip_atomic_store((gu32*)prog, 0x51000000u | (code & 0xff) << 8 | (nit & 0xff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -965,6 +1223,10 @@ hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStrea
       if (bits != 4) return hipErrorInvalidValue;
       hipLaunchKernelGGL(nw_align_affine, dim3(grid), dim3(256), 0, s, a);
       return hipGetLastError();
+    case kPacked:
+      if (bits != 4) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(nw_align_pk, dim3(grid), dim3(256), 0, s, a);
+      return hipGetLastError();
     case kProfile: return fill_m<kProfile>(bits, a, grid, s);
     case kCompare: return fill_m<kCompare>(bits, a, grid, s);
     case kLiteral: return bits == 32 ? fill_w<kLiteral, 32>(a, grid, s) : hipErrorInvalidValue;
@@ -982,10 +1244,10 @@ static int occ_w() {
 
 int fill_blocks_per_cu(int mode, int bits) {
   if (mode == kLiteral) return occ_w<kLiteral, 32>();
-  if (mode == kAffine) {
+  if (mode == kAffine || mode == kPacked) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&nw_align_affine), 256, 0) != hipSuccess)
-      return 1;
+    const void* f = mode == kAffine ? reinterpret_cast<const void*>(&nw_align_affine) : reinterpret_cast<const void*>(&nw_align_pk);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 256, 0) != hipSuccess) return 1;
     return n > 0 ? n : 1;
   }
   const bool p = mode == kProfile;

@@ -142,6 +142,8 @@ struct nwk_ctx {
   DevBuf d_codes[2];            // [0] profile codes, [1] raw bytes
   DevBuf d_E[2];
   bool built[2] = {false, false};
+  DevBuf d_sel[2];              // kPacked selector streams: [0] hi = 0x00, [1] hi = 0xff
+  bool built_sel[2] = {false, false};
 
   // batch buffers
   DevBuf d_work;                // matrices | boundary granules | op strings
@@ -174,6 +176,7 @@ void nwk_ctx_destroy(nwk_ctx* c) {
   (void)hipSetDevice(c->device);
   for (auto& b : c->d_codes) b.release();
   for (auto& b : c->d_E) b.release();
+  for (auto& b : c->d_sel) b.release();
   c->d_work.release();
   c->d_pairs.release(); c->d_tasks.release(); c->d_ctl.release();
   c->d_oplen.release(); c->d_endij.release(); c->d_done.release(); c->d_stamps.release();
@@ -240,7 +243,8 @@ int nwk_set_sequences(nwk_ctx* c, const uint8_t* seqs, const int64_t* offsets, i
   for (int b = 0; b < 256; ++b)
     if (seen[b]) c->code_of[b] = (uint8_t)c->alpha++;
   c->built[0] = c->built[1] = false;
-  // layout: codes 8-aligned; E with kEPad entries before column 0 and 256 after the end
+  c->built_sel[0] = c->built_sel[1] = false;
+  // layout: codes 8-aligned; E / SEL with kEPad entries before column 0 and kETail past the end
   c->c_off.resize(k);
   c->e_off.resize(k);
   int64_t co = kCodesFrontPad, eo = 0;
@@ -249,7 +253,7 @@ int nwk_set_sequences(nwk_ctx* c, const uint8_t* seqs, const int64_t* offsets, i
     c->c_off[s] = co;
     co += round_up(L + 8, 8);
     c->e_off[s] = eo + kEPad;
-    eo += kEPad + L + 256;
+    eo += kEPad + L + kETail;
   }
   return NWK_OK;
 }
@@ -266,7 +270,7 @@ int build_encoding(nwk_ctx* c, int kind) {
   const int k = c->k;
   const int64_t ncodes =
       (k ? c->c_off[k - 1] + round_up(c->off[k] - c->off[k - 1] + 8, 8) : kCodesFrontPad) + kCodesTailPad;
-  const int64_t nE = k ? c->e_off[k - 1] - kEPad + kEPad + (c->off[k] - c->off[k - 1]) + 256 : 64;
+  const int64_t nE = k ? c->e_off[k - 1] + (c->off[k] - c->off[k - 1]) + kETail : 64;
   std::vector<uint8_t> codes((size_t)ncodes, 0);
   std::vector<uint32_t> E((size_t)nE, 0);
   for (int s = 0; s < k; ++s) {
@@ -275,7 +279,7 @@ int build_encoding(nwk_ctx* c, int kind) {
     uint8_t* cd = codes.data() + c->c_off[s];
     for (int64_t a = 0; a < L; ++a) cd[a] = kind == 0 ? c->code_of[y[a]] : y[a];
     uint32_t* e = E.data() + c->e_off[s];
-    for (int64_t a = -kEPad; a < L + 256 - kEPad; ++a) {
+    for (int64_t a = -kEPad; a < L + kETail; ++a) {
       uint32_t v = 0;
       for (int q = 0; q < 4; ++q) {
         const int64_t t = a + q;
@@ -292,6 +296,30 @@ int build_encoding(nwk_ctx* c, int kind) {
   HIP_TRY(hipMemcpy(c->d_codes[kind].p, codes.data(), codes.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(c->d_E[kind].p, E.data(), E.size() * 4, hipMemcpyHostToDevice));
   c->built[kind] = true;
+  return NWK_OK;
+}
+
+// kPacked selector stream (same indexing as E): SEL[a] = {code(y[a]), hi,
+// 4 + code(y[a-1]), hi} -- the v_perm selector of the substitution profile
+// bytes of a row pair at column a+1 (row q) and a (row q+4); hi = 0x0d
+// (byte 0xff: both K < 0) or 0x0c (byte 0x00: both K >= 0) sign-extends.
+int build_sel(nwk_ctx* c, int neg) {
+  if (c->built_sel[neg]) return NWK_OK;
+  const int k = c->k;
+  const int64_t nE = k ? c->e_off[k - 1] + (c->off[k] - c->off[k - 1]) + kETail : 64;
+  std::vector<uint32_t> S((size_t)nE, 0);
+  const uint32_t hi = neg ? 0x0du : 0x0cu;
+  for (int s = 0; s < k; ++s) {
+    const uint8_t* y = c->seqs.data() + c->off[s];
+    const int64_t L = c->off[s + 1] - c->off[s];
+    uint32_t* e = S.data() + c->e_off[s];
+    auto code = [&](int64_t t) -> uint32_t { return t >= 0 && t < L ? c->code_of[y[t]] : 0u; };
+    for (int64_t a = -kEPad; a < L + kETail; ++a) e[a] = code(a) | hi << 8 | (4u + code(a - 1)) << 16 | hi << 24;
+  }
+  int rc;
+  if ((rc = c->d_sel[neg].ensure(S.size() * 4)) != NWK_OK) return rc;
+  HIP_TRY(hipMemcpy(c->d_sel[neg].p, S.data(), S.size() * 4, hipMemcpyHostToDevice));
+  c->built_sel[neg] = true;
   return NWK_OK;
 }
 
@@ -333,13 +361,21 @@ int choose_plan(const nwk_ctx* c, const Scoring& sc, Plan* pl) {
   pl->kind = pl->mode == kProfile ? 0 : 1;
   pl->K0 = (int)(-2 * (int64_t)pgap);
   pl->K1 = (int)((int64_t)pxy - 2 * (int64_t)pgap);
+  // two cells per register when the profile bytes sign-extend uniformly
+  // (K0, K1 both < 0 or both >= 0); NWK_PACKED=0 keeps nw_align (A/B)
+  static const bool packed_off = getenv("NWK_PACKED") && atoi(getenv("NWK_PACKED")) == 0;
+  if (pl->mode == kProfile && pl->bits == 4 && !packed_off && ((pl->K0 < 0) == (pl->K1 < 0))) pl->mode = kPacked;
   return NWK_OK;
 }
 
-void footprint(PairWork* w, int bits, bool affine) {
+// 64-step super-blocks per band: the last band-row value of column n leaves
+// lane 63 at step n + 62 (nw_align) or n + 126 (nw_align_pk, 2-column skew).
+inline int sblocks_of(int mode, int64_t nch) { return (int)(nch + (mode == kPacked ? 2 : 1)); }
+
+void footprint(PairWork* w, int bits, int mode, bool affine) {
   const int64_t nb = ceil_div(w->m, kBandRows);
   const int64_t nch = ceil_div(w->n, 64);
-  w->mat_dw = nb * band_dwords(bits, (int)(nch + 1));
+  w->mat_dw = nb * band_dwords(bits, sblocks_of(mode, nch));
   w->bnd_gr = (nb - 1) * nch * 64 * (affine ? 2 : 1);  // affine: H and F boundary rows
   w->ops_b = round_up((int64_t)w->m + w->n, 16);
 }
@@ -479,12 +515,13 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       memcpy(hashes + 64 * w.out, f.hash, 64);
       if (chain) chain->ready[w.out] = 1;
     } else {
-      footprint(&w, pl.bits, sc.affine);
+      footprint(&w, pl.bits, pl.mode, sc.affine);
       dp.push_back(w);
     }
   }
   if (!dp.empty()) {
     if ((rc = build_encoding(c, pl.kind)) != NWK_OK) return rc;
+    if (pl.mode == kPacked && (rc = build_sel(c, pl.K0 < 0 ? 1 : 0)) != NWK_OK) return rc;
   }
   // Largest first (LPT inside the device; longest bands dequeued first).
   std::sort(dp.begin(), dp.end(), [](const PairWork& a, const PairWork& b) {
@@ -554,7 +591,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       d.n = w.n;
       d.nbands = (int)ceil_div(w.m, kBandRows);
       d.nchunks = (int)ceil_div(w.n, 64);
-      d.sblocks = d.nchunks + 1;
+      d.sblocks = sblocks_of(pl.mode, d.nchunks);
       d.slot = q;
       mo += w.mat_dw; bo += w.bnd_gr; oo += w.ops_b;
       ntasks += d.nbands;
@@ -603,6 +640,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.ntasks = (int)ntasks;
     fa.codes = c->d_codes[pl.kind].as<uint8_t>();
     fa.E = c->d_E[pl.kind].as<uint32_t>();
+    fa.sel = pl.mode == kPacked ? c->d_sel[pl.K0 < 0 ? 1 : 0].as<uint32_t>() : nullptr;
     fa.mat = c->d_work.as<uint32_t>();
     fa.bnd = c->d_work.as<unsigned long long>();
     fa.counter = c->d_ctl.as<unsigned>();
