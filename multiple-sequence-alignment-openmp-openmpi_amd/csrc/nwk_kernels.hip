@@ -228,14 +228,18 @@ template <int W, bool PK = false>
 struct TbConf {
   using L = Lay<W, PK>;
   static constexpr int SPC = L::SPC;
-  static constexpr int TC = PK ? 16 : 8;            // column units per window
+  static constexpr int TC = PK ? 32 : 8;            // column units per window
   static constexpr int TS = TC * SPC;               // steps per window
   // column units below the window: a block reaches 10 (plain) / 12 (packed) steps below its cell
   static constexpr int OV = PK ? 4 : (11 + SPC - 1) / SPC;
   static constexpr int CC = TC + OV;
   static constexpr int TL = 16;                     // lanes (8-row groups) per tile
   static constexpr int TILE = CC * L::RPC * TL;     // dwords
-  static constexpr int NB = 1;                       // single buffer: LDS per block bounds fill occupancy
+#ifndef NWK_PK_TB_NB
+#define NWK_PK_TB_NB 1
+#endif
+  // tile buffers: 1 (LDS per block bounds the plain kernels' fill occupancy) or 2 (next window prefetched)
+  static constexpr int NB = PK ? NWK_PK_TB_NB : 1;
   static constexpr int YLO = 96;                    // plain: y window starts 96 columns below the window
   static_assert(TILE % 64 == 0, "tile = whole DMA instructions");
   static_assert(L::RPC % 4 == 0, "a DMA covers 4 dword rows x 16 lanes");
@@ -300,7 +304,7 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
   const uint8_t* yg = a.codes + pd.y_off;
   const unsigned* mb = a.mat + pd.mat_off;
   const bool prof = a.stamps != nullptr;
-  unsigned long long cy_sw = 0, cy_blk = 0, n_blk = 0, n_sw = 0, n_sync = 0, tA = 0, tB;
+  unsigned long long cy_sw = 0, cy_blk = 0, cy_walk = 0, n_blk = 0, n_sw = 0, tA = 0, tB;
 
   // Stage tile (b, q, t0) into buffer buf by LDS-DMA: lanes [t0, t0+16) of
   // band b, column units [TC*q - OV, TC*q + TC) (clamped), the x codes of
@@ -355,12 +359,11 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
         const int q = s / C::TS;
         drain();
         n_sw++;
-        flush(Lc & ~3);  // stores issued right after a drain have a whole tile to land
         if (C::NB == 2 && b == pb && q == pq && tl >= pt0 && t < pt0 + C::TL) {
           cur ^= 1;
           tt0 = pt0;
         } else {
-          n_sync++;
+
           const int nt0 = max(0, t - (C::TL - 3));
           const int nbuf = C::NB == 2 ? (cur ^ 1) : 0;
           issue(nbuf, b, q, nt0);
@@ -368,6 +371,7 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
           cur = nbuf;
           tt0 = nt0;
         }
+        flush(Lc & ~3);  // issued after the tile landed: the stores drain during this window's walk
         tb = b;
         tq = q;
         yw = C::ywin(q, tt0);
@@ -457,31 +461,34 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
     const unsigned gd = bd ? 0u : (vd >> shd) & MASK;
     const bool isD = (vx & 0xffu) == (vy & 0xffu) || ((gd + (unsigned)a.K1 - g) & MASK) == 0u;
     const bool isU = !isD && ((gu - g) & MASK) == 0u;
-    // ---- the walk: each lane packs its cell's move (ASCII) and successor
-    // lane (64 = leaves the block or reaches the border); the walk is a chain
-    // of v_readlane with a scalar lane index, one uniform byte store per step.
+    // ---- the walk: each lane packs its cell's move (ASCII, low byte: the
+    // byte store takes it as is) and successor lane (64 = leaves the block or
+    // reaches the border); the walk is a chain of v_readlane with a scalar
+    // lane index, one byte store per step.
     const int nli = li + (isD || isU ? 1 : 0), nlj = lj + (isU ? 0 : 1);
     const bool leaves = nli > 7 || nlj > 7 || i - nli <= 0 || j - nlj <= 0;
-    const unsigned code = ((isD ? (unsigned)'D' : isU ? (unsigned)'U' : (unsigned)'L') << 8) |
-                          (leaves ? 64u : (unsigned)(nli * 8 + nlj));
+    const unsigned code = (isD ? (unsigned)'D' : isU ? (unsigned)'U' : (unsigned)'L') |
+                          ((leaves ? 64u : (unsigned)(nli * 8 + nlj)) << 8);
+    unsigned long long tW = prof ? __builtin_amdgcn_s_memtime() : 0;
     unsigned curl = 0, last = 0, cw = 0;
     do {
       last = curl;
       cw = __builtin_amdgcn_readlane(code, curl);
-      asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(cw >> 8) : "memory");
+      asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(cw) : "memory");
       ++Lc;
-      curl = cw & 0xffu;
+      curl = cw >> 8;
     } while (curl < 64u);
+    if (prof) cy_walk += __builtin_amdgcn_s_memtime() - tW;
     if (Lc - flushed >= 160) flush(Lc & ~3);  // ring of 256, a block adds <= 15: never overrun
     // the last cell visited and its move give the block's total displacement
-    const unsigned op = cw >> 8;
+    const unsigned op = cw & 0xffu;
     i -= (int)(last >> 3) + (op != 'L' ? 1 : 0);
     j -= (int)(last & 7u) + (op != 'U' ? 1 : 0);
     if (prof) { tB = __builtin_amdgcn_s_memtime(); cy_blk += tB - tA; }
   }
   if (prof && lane == 0) {
     unsigned long long* st = a.stamps + 8 * pd.slot + 2;
-    st[0] = cy_sw; st[1] = cy_blk; st[2] = n_blk; st[3] = (n_sw << 32) | n_sync;
+    st[0] = cy_sw; st[1] = cy_blk; st[2] = n_blk; st[3] = (n_sw << 32) | (cy_walk & 0xffffffffull);  // diagnostics: walk cycles in the low half
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   flush(Lc);
@@ -797,13 +804,22 @@ __global__ __launch_bounds__(256) void nw_align_pk(FillArgs a) {
     wait_vm_keep3<0>(sw0, sw1, sw2, pend);
     bool ok = true;
     constexpr int kBlockStores = 8;
+    u64 cyc_wait = 0, cyc_wait0 = 0, n_wait = 0;
+    const u64 t_task = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
 
     for (int sb = 0; sb < pd.sblocks; ++sb) {
       // --- band-above row for this super-block: B[64sb+1 .. 64sb+64] = chunk sb
       int bval = 0;
       if (from_above && sb < pd.nchunks) {
         if (!__all((unsigned)(pend >> 32) == a.epoch)) {
+          const u64 tw = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
           pend = wait_granules(gin + 64 * sb, a.epoch, pend, a.err);
+          if (a.stamps) {
+            const u64 d = __builtin_amdgcn_s_memtime() - tw;
+            cyc_wait += d;
+            if (sb == 0) cyc_wait0 += d;
+            ++n_wait;
+          }
           if (!__all((unsigned)(pend >> 32) == a.epoch)) { ok = false; break; }
         }
         bval = (int)(unsigned)pend;
@@ -849,13 +865,26 @@ __global__ __launch_bounds__(256) void nw_align_pk(FillArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.stamps && lane == 0) {  // per pair: band cycles, of which waiting on the band above
+      atomicAdd(a.stamps + 8 * pd.slot + 6, (unsigned long long)(__builtin_amdgcn_s_memtime() - t_task));
+      atomicAdd(a.stamps + 8 * pd.slot + 7, (unsigned long long)cyc_wait);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot, (unsigned long long)cyc_wait0);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 1, (unsigned long long)n_wait);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 2, (unsigned long long)pd.sblocks);
+    }
     unsigned prev = 0;
     if (lane == 0) prev = __hip_atomic_fetch_add((gu32*)(a.done + pd.slot), 1u, RLX_AGENT);
     prev = __builtin_amdgcn_readfirstlane(prev);
     if (prev + 1u == (unsigned)pd.nbands) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      trace_pair<W, true>(a, pd, tbl[wid], lane);
+      if (a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
+      if (a.dbg_notrace) {  // debug (NWK_NOTRACE): fill-only timing, results invalid
+        if (lane == 0) { a.oplen[pd.slot] = 0; a.endij[pd.slot] = make_int2(pd.m, pd.n); }
+      } else {
+        trace_pair<W, true>(a, pd, tbl[wid], lane);
+      }
+      if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
     }
   }
 }

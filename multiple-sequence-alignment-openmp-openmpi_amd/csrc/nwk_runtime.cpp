@@ -529,7 +529,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     if (ca != cb) return ca > cb;
     return a.id < b.id;
   });
-  const int bpc = fill_blocks_per_cu(pl.mode, pl.bits);
+  int bpc = fill_blocks_per_cu(pl.mode, pl.bits);
+  static const int bpc_cap = getenv("NWK_BPC") ? atoi(getenv("NWK_BPC")) : 0;  // experiment: waves per SIMD
+  if (bpc_cap > 0 && bpc_cap < bpc) bpc = bpc_cap;
   const int grid = bpc * c->cus;
   float ms = 0;
 
@@ -651,7 +653,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.K0 = pl.K0;
     fa.K1 = pl.K1;
     fa.go = sc.go;
-    fa.dbg_notrace = getenv("NWK_AFF_NOTRACE") ? 1 : 0;
+    fa.dbg_notrace = (getenv("NWK_AFF_NOTRACE") || getenv("NWK_NOTRACE")) ? 1 : 0;
     fa.prog = nullptr;
     if (getenv("NWK_WATCHDOG")) {
       if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;
@@ -729,7 +731,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       unsigned long long t0 = ~0ull;
       for (int q = 0; q < np; ++q) t0 = std::min(t0, sp[8 * q]);
       fprintf(stderr, "nwk timeline (ms after first pair filled; kernel %.3f ms): pair m x n: filled -> traced | "
-                      "trace cycles switch/blocks, blocks, switches/sync | fill band-cycles, %% waiting on band above\n", ms);
+                      "trace cycles switch/blocks, blocks, switches/walk-cycles | fill band-cycles, %% waiting on band above\n", ms);
       double bc = 0, wc = 0;
       for (int q = 0; q < np; ++q) {
         const unsigned long long* x = &sp[8 * q];
