@@ -68,7 +68,7 @@ typedef struct nwk_stats {
   int64_t matrix_bytes;      /* HBM bytes of the stored DP matrices */
   int32_t batches;           /* workspace batches used */
   int32_t bits;              /* storage width used */
-  int32_t mode;              /* 0 = profile, 1 = compare, 2 = literal, 3 = affine, 4 = packed profile */
+  int32_t mode;              /* 0 = profile, 1 = compare, 2 = literal, 3 = affine, 4 = packed profile, 5 = packed band pairs */
   int32_t fill_launches;     /* fill-kernel launches in the call */
   int32_t reserved[4];
 } nwk_stats;

@@ -23,6 +23,7 @@ enum Mode : int {
   kLiteral = 2,  // any penalties: skel:215-224 literally (match ? diag : min3)
   kAffine = 3,   // affine gaps: 4-bit traceback codes, compare mode
   kPacked = 4,   // kProfile at W = 4 with two cells per register (int16 pairs), packed layout
+  kPacked2 = 5,  // kPacked with two bands per wave (band pairs), layout LY 2
 };
 
 // One pair of the batch.  All offsets are element offsets into the
@@ -39,6 +40,11 @@ struct PairDesc {
   int32_t nchunks;  // ceil(n / 64): 64-column boundary chunks
   int32_t sblocks;  // 64-step super-blocks per band = nchunks + 1 (kPacked: + 2)
   int32_t slot;     // index of this pair in the batch's result arrays
+  // kPacked2 segmented traceback (see nw_align_pk2 / nw_gather)
+  int32_t spec_every;   // a speculative segment after every spec_every-th task (0: whole-pair trace)
+  int64_t task_off;     // first entry of this pair in tdone / seginfo (one per task)
+  int64_t rec_off;      // first record of this pair in recs ([m / 128 + 1][2])
+  int64_t segops_off;   // first byte of this pair's segment move buffers in segops
 };
 
 struct FillArgs {
@@ -47,7 +53,7 @@ struct FillArgs {
   int ntasks;
   const uint8_t* codes;    // sequence codes (x rows, y columns)
   const uint32_t* E;       // expanded column codes, 4 per dword
-  const uint32_t* sel;     // kPacked: per column v_perm selector {y[a], hi, 4+y[a-1], hi}
+  const uint32_t* sel;     // kPacked: per column v_perm selector {y[a], hi, 4+y[a-1], hi}; kPacked2: {y[a], hi, 4+y[a-64], hi}
   uint32_t* mat;           // packed G = H - (i+j)*pgap, W bits per cell
   unsigned long long* bnd; // {epoch:32 | G:32} granules, one per boundary cell
   unsigned* counter;       // task dequeue head
@@ -63,10 +69,17 @@ struct FillArgs {
   int go, ge;              // kAffine: gap open / extend
   int dbg_notrace;         // debug: skip the affine traceback
   unsigned* prog;          // debug: per-wave progress markers (NWK_WATCHDOG)
+  unsigned* tdone;         // kPacked2: per task, 1 = filled and released
+  int* seginfo;            // kPacked2: per task, 8 ints {len, ei, ej, mseg, midx, off lo, off hi, -}
+  unsigned long long* recs;  // kPacked2: traceback record rows
+  uint8_t* segops;         // kPacked2: segment move buffers
 };
+
+constexpr int kMaxTasksPerPair = 2048;  // kPacked2 segment ids are 11 bits (m <= 2^21 rows)
 
 // Launchers (nwk_kernels.hip).  bits in {4, 8, 16, 32}.
 hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStream_t s);
+hipError_t launch_gather(const FillArgs& a, int npairs, hipStream_t s);
 int fill_blocks_per_cu(int mode, int bits);
 
 // Dwords of one band of the stored matrix.

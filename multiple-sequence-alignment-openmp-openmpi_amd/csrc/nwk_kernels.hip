@@ -199,39 +199,58 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const lds_u32*)p;
 }
 
-// Stored-matrix layouts.
-//  plain  (nw_align, W bits):  per band, dword (c*8 + r)*64 + t holds row r of
-//         lane t for steps [c*SPD, (c+1)*SPD), SPD = 32/W; cell (row 8t+r,
-//         column j) is step s = j-1+t, bits W*(s%SPD).
-//  packed (nw_align_pk, W = 4): dword (g*4 + q)*64 + t holds rows q and q+4
-//         of lane t for steps [4g, 4g+4); cell (8t+r, j) is step
-//         s = j-1+2t+h (h = r>>2: rows 4..7 run one column behind rows 0..3),
-//         nibble at bit 8*(2*(s&1)+h) + 4*((s>>1)&1).
-template <int W, bool PK>
+// Stored-matrix layouts (LY).
+//  0 plain  (nw_align, W bits):  per band, dword (c*8 + r)*64 + t holds row r of
+//           lane t for steps [c*SPD, (c+1)*SPD), SPD = 32/W; cell (row 8t+r,
+//           column j) is step s = j-1+t, bits W*(s%SPD).
+//  1 packed (nw_align_pk, W = 4): dword (g*4 + q)*64 + t holds rows q and q+4
+//           of lane t for steps [4g, 4g+4); cell (8t+r, j) is step
+//           s = j-1+2t+h (h = r>>2: rows 4..7 run one column behind rows
+//           0..3), nibble at bit 8*(2*(s&1)+h) + 4*((s>>1)&1).
+//  2 band pairs (nw_align_pk2, W = 4): bands 2p and 2p+1 share one region of
+//           2 band_dwords; dword (g*8 + r)*64 + t holds row r of lane t of
+//           both bands for steps [4g, 4g+4); cell (8t+r, j) of band 2p+h is
+//           step s = j-1+t+64h (the odd band runs 64 columns behind), nibble
+//           at bit 8*(2*(s&1)+h) + 4*((s>>1)&1).
+template <int W, int LY>
 struct Lay {
   static constexpr int SPC = 32 / W;  // steps per column unit
   static constexpr int RPC = kRows;   // dwords per column unit per lane
-  __device__ static int step(int t, int r, int j) { (void)r; return j - 1 + t; }
+  __device__ static int hb(int b) { (void)b; return 0; }
+  __device__ static int64_t base(int b, int64_t bdw) { return (int64_t)b * bdw; }
+  __device__ static int step(int t, int r, int j, int h) { (void)r; (void)h; return j - 1 + t; }
   __device__ static int slot(int r) { return r; }
-  __device__ static int shift(int s, int r) { (void)r; return W == 32 ? 0 : W * (s & (SPC - 1)); }
+  __device__ static int shift(int s, int r, int h) { (void)r; (void)h; return W == 32 ? 0 : W * (s & (SPC - 1)); }
 };
 template <>
-struct Lay<4, true> {
+struct Lay<4, 1> {
   static constexpr int SPC = 4;
   static constexpr int RPC = 4;
-  __device__ static int step(int t, int r, int j) { return j - 1 + 2 * t + (r >> 2); }
+  __device__ static int hb(int b) { (void)b; return 0; }
+  __device__ static int64_t base(int b, int64_t bdw) { return (int64_t)b * bdw; }
+  __device__ static int step(int t, int r, int j, int h) { (void)h; return j - 1 + 2 * t + (r >> 2); }
   __device__ static int slot(int r) { return r & 3; }
-  __device__ static int shift(int s, int r) { return 8 * (2 * (s & 1) + (r >> 2)) + 4 * ((s >> 1) & 1); }
+  __device__ static int shift(int s, int r, int h) { (void)h; return 8 * (2 * (s & 1) + (r >> 2)) + 4 * ((s >> 1) & 1); }
+};
+template <>
+struct Lay<4, 2> {
+  static constexpr int SPC = 4;
+  static constexpr int RPC = kRows;
+  __device__ static int hb(int b) { return b & 1; }
+  __device__ static int64_t base(int b, int64_t bdw) { return (int64_t)(b >> 1) * 2 * bdw; }
+  __device__ static int step(int t, int r, int j, int h) { (void)r; return j - 1 + t + 64 * h; }
+  __device__ static int slot(int r) { return r; }
+  __device__ static int shift(int s, int r, int h) { (void)r; return 8 * (2 * (s & 1) + h) + 4 * ((s >> 1) & 1); }
 };
 
-template <int W, bool PK = false>
+template <int W, int LY = 0>
 struct TbConf {
-  using L = Lay<W, PK>;
+  using L = Lay<W, LY>;
   static constexpr int SPC = L::SPC;
-  static constexpr int TC = PK ? 32 : 8;            // column units per window
+  static constexpr int TC = LY == 1 ? 32 : LY == 2 ? 16 : 8;  // column units per window
   static constexpr int TS = TC * SPC;               // steps per window
-  // column units below the window: a block reaches 10 (plain) / 12 (packed) steps below its cell
-  static constexpr int OV = PK ? 4 : (11 + SPC - 1) / SPC;
+  // column units below the window: a block reaches 10 (plain, LY 2) / 12 (LY 1) steps below its cell
+  static constexpr int OV = LY == 1 ? 4 : (11 + SPC - 1) / SPC;
   static constexpr int CC = TC + OV;
   static constexpr int TL = 16;                     // lanes (8-row groups) per tile
   static constexpr int TILE = CC * L::RPC * TL;     // dwords
@@ -239,38 +258,44 @@ struct TbConf {
 #define NWK_PK_TB_NB 1
 #endif
   // tile buffers: 1 (LDS per block bounds the plain kernels' fill occupancy) or 2 (next window prefetched)
-  static constexpr int NB = PK ? NWK_PK_TB_NB : 1;
+  static constexpr int NB = LY ? NWK_PK_TB_NB : 1;
   static constexpr int YLO = 96;                    // plain: y window starts 96 columns below the window
   static_assert(TILE % 64 == 0, "tile = whole DMA instructions");
   static_assert(L::RPC % 4 == 0, "a DMA covers 4 dword rows x 16 lanes");
-  static_assert(PK || TS + YLO <= 256, "y window must fit one DMA");
-  static_assert(PK ? (TS + 56 <= 256 && 2 * 63 + 48 + 3 <= kCodesFrontPad) : YLO <= kCodesFrontPad,
-                "y windows must stay inside the codes buffer");
-  // first y column (0-based) of the 256-byte window staged for step window q, lanes [t0, t0+16)
-  __device__ static int ywin(int q, int t0) { return PK ? ((TS * q - 2 * t0 - 48) & ~3) : TS * q - YLO; }
+  static_assert(LY || TS + YLO <= 256, "y window must fit one DMA");
+  static_assert(LY != 1 || (TS + 56 <= 256 && 2 * 63 + 48 + 3 <= kCodesFrontPad), "y window (LY 1)");
+  static_assert(LY != 2 || (TS + 64 <= 256 && 63 + 64 + 48 + 3 <= kCodesFrontPad), "y window (LY 2)");
+  static_assert(LY || YLO <= kCodesFrontPad, "y windows must stay inside the codes buffer");
+  // first y column (0-based) of the 256-byte window staged for step window q, lanes [t0, t0+16), half h
+  __device__ static int ywin(int q, int t0, int h) {
+    if constexpr (LY == 1) return (TS * q - 2 * t0 - 48) & ~3;
+    else if constexpr (LY == 2) return (TS * q - t0 - 64 * h - 48) & ~3;
+    else { (void)t0; (void)h; return TS * q - YLO; }
+  }
 };
 
-template <int W, bool PK = false>
+template <int W, int LY = 0>
 struct TbLds {
-  unsigned tile[TbConf<W, PK>::NB][TbConf<W, PK>::TILE];
-  unsigned xs[TbConf<W, PK>::NB][64];
-  unsigned ys[TbConf<W, PK>::NB][64];
+  unsigned tile[TbConf<W, LY>::NB][TbConf<W, LY>::TILE];
+  unsigned xs[TbConf<W, LY>::NB][64];
+  unsigned ys[TbConf<W, LY>::NB][64];
   unsigned obuf[64];   // 256-byte ring of traceback moves, flushed to HBM in dwords
 };
 
-template <int W, bool PK = false>
+template <int W, int LY = 0>
 __device__ __forceinline__ unsigned getG_global(const unsigned* M, const PairDesc& pd, int64_t bdw, int i, int j) {
   if (i == 0 || j == 0) return 0u;
-  using L = Lay<W, PK>;
+  using L = Lay<W, LY>;
   const int w = i - 1;
   const int b = w / kBandRows;
   const int wr = w - b * kBandRows;
   const int t = wr / kRows;
   const int r = wr - t * kRows;
-  const int s = L::step(t, r, j);
-  const unsigned d = M[pd.mat_off + (int64_t)b * bdw + ((int64_t)(s / L::SPC) * L::RPC + L::slot(r)) * kWave + t];
+  const int h = L::hb(b);
+  const int s = L::step(t, r, j, h);
+  const unsigned d = M[pd.mat_off + L::base(b, bdw) + ((int64_t)(s / L::SPC) * L::RPC + L::slot(r)) * kWave + t];
   if constexpr (W == 32) return d;
-  else return (d >> L::shift(s, r)) & ((1u << W) - 1u);
+  else return (d >> L::shift(s, r, h)) & ((1u << W) - 1u);
 }
 
 struct Five { unsigned v[5]; };
@@ -278,23 +303,48 @@ struct Five { unsigned v[5]; };
 // Rare cells (band above, outside the staged window) come from global memory
 // in a non-inlined call, so the wait for those loads -- which also drains the
 // tile prefetch -- stays on this path.
-template <int W, bool PK>
+template <int W, int LY>
 __device__ __noinline__ Five tb_fallback(const unsigned* mat, const PairDesc& pd, int64_t bdw, const uint8_t* xg,
                                          const uint8_t* yg, int ci, int cj, bool fx, bool fy, bool fg, bool fu,
                                          bool fd, int shg, int shu, int shd, Five in) {
   Five o = in;
   if (fx) o.v[0] = xg[ci - 1];
   if (fy) o.v[1] = yg[cj - 1];
-  if (fg) o.v[2] = getG_global<W, PK>(mat, pd, bdw, ci, cj) << shg;
-  if (fu) o.v[3] = getG_global<W, PK>(mat, pd, bdw, ci - 1, cj) << shu;
-  if (fd) o.v[4] = getG_global<W, PK>(mat, pd, bdw, ci - 1, cj - 1) << shd;
+  if (fg) o.v[2] = getG_global<W, LY>(mat, pd, bdw, ci, cj) << shg;
+  if (fu) o.v[3] = getG_global<W, LY>(mat, pd, bdw, ci - 1, cj) << shu;
+  if (fd) o.v[4] = getG_global<W, LY>(mat, pd, bdw, ci - 1, cj - 1) << shd;
   return o;
 }
 
-template <int W, bool PK = false>
-__device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd, TbLds<W, PK>& L, int lane) {
-  using C = TbConf<W, PK>;
-  using Y = Lay<W, PK>;
+// A traceback segment.  The whole-pair trace starts at (m, n) with no
+// records.  Speculative segments (nw_align_pk2) start on a task boundary row;
+// every segment stops its walk on each record row (multiple of kRecRows) and
+// there claims or matches a per-row record {column, segment, move index}: a
+// match means the two paths are identical from that cell on, so the segment
+// ends with a merge link (SegOut.mseg / midx) that the gather kernel follows.
+struct SegCtx {
+  uint8_t* ops;                    // this segment's move buffer (reversed moves)
+  int i0, j0;                      // start cell
+  int seg;                         // segment id (task index) for records
+  unsigned long long* recs;        // per pair [m / kRecRows + 1][2] records, nullptr: none
+  const unsigned* tdone;           // per pair task-done flags, nullptr: all done
+  int task_shift;                  // band -> task: b >> task_shift
+};
+struct SegOut {
+  int len, ei, ej;                 // moves, end cell
+  int mseg, midx;                  // merged into segment mseg at its move midx (-1: ran to the border)
+};
+constexpr int kRecRows = 128;
+// record: bit 63 valid | column << 41 | segment << 30 | move index
+__device__ __forceinline__ unsigned long long rec_pack(int col, int seg, int idx) {
+  return (1ull << 63) | ((unsigned long long)col << 41) | ((unsigned long long)seg << 30) | (unsigned long long)idx;
+}
+
+template <int W, int LY = 0>
+__device__ __forceinline__ SegOut trace_pair(const FillArgs& a, const PairDesc& pd, TbLds<W, LY>& L, int lane,
+                                             const SegCtx& sc) {
+  using C = TbConf<W, LY>;
+  using Y = Lay<W, LY>;
   constexpr int SPC = Y::SPC;
   constexpr int RPC = Y::RPC;
   constexpr unsigned MASK = W == 32 ? 0xffffffffu : ((1u << (W & 31)) - 1u);
@@ -313,7 +363,7 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
   // lanes t0 + lane%16.
   const int lane_off = (lane >> 4) * kWave + (lane & 15);
   auto issue = [&](int buf, int b, int q, int t0) {
-    const unsigned* src = mb + (int64_t)b * bdw + t0 + lane_off;
+    const unsigned* src = mb + Y::base(b, bdw) + t0 + lane_off;
 #pragma unroll
     for (int k = 0; k < C::TILE / 64; ++k) {
       int c = C::TC * q - C::OV + k / (RPC / 4);
@@ -323,15 +373,16 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
     }
     const unsigned* xsrc = reinterpret_cast<const unsigned*>(xg + (int64_t)b * kBandRows + 8 * t0);
     __builtin_amdgcn_global_load_lds((gbl_void*)(xsrc + lane), (lds_void*)&L.xs[buf][0], 4, 0, 0);
-    const unsigned* ysrc = reinterpret_cast<const unsigned*>(yg + C::ywin(q, t0));
+    const unsigned* ysrc = reinterpret_cast<const unsigned*>(yg + C::ywin(q, t0, Y::hb(b)));
     __builtin_amdgcn_global_load_lds((gbl_void*)(ysrc + lane), (lds_void*)&L.ys[buf][0], 4, 0, 0);
   };
   // The walk reads LDS only through inline asm, so the compiler does not
   // make every read wait for the in-flight DMA: this drain is the one wait.
   auto drain = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
 
-  uint8_t* ops = a.ops + pd.ops_off;
-  int i = pd.m, j = pd.n, Lc = 0, flushed = 0;
+  uint8_t* ops = sc.ops;
+  int i = sc.i0, j = sc.j0, Lc = 0, flushed = 0;
+  int mseg = -1, midx = 0, last_rec = -1, task_ok = 1 << 30;  // tasks >= task_ok are known done
   int tb = -1, tq = 0, tt0 = 0, cur = 0, pb = -1, pq = 0, pt0 = 0, yw = 0;
   const unsigned ob = lds_addr(&L.obuf[0]);
   // Moves go to an LDS ring (ds_write_b8, no VMEM) and reach HBM as whole
@@ -349,14 +400,50 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
 
   while (i > 0 && j > 0) {
     if (prof) tA = __builtin_amdgcn_s_memtime();
+    if (sc.recs && (i & (kRecRows - 1)) == 0 && i != last_rec) {  // arrived on a record row
+      last_rec = i;
+      unsigned long long* rp = sc.recs + 2 * (i / kRecRows);
+      int hit = -1;
+      unsigned long long v0 = 0;
+      if (lane == 0) {
+        const unsigned long long mine = rec_pack(j, sc.seg, Lc);
+        for (int k = 0; k < 2 && hit < 0; ++k) {
+          unsigned long long v = __hip_atomic_load((gu64*)(rp + k), RLX_AGENT);
+          if (v == 0) {
+            v = atomicCAS((unsigned long long*)(rp + k), 0ull, mine);
+            if (v == 0) { hit = 2; break; }  // claimed: this segment owns the row's slot k
+          }
+          if ((int)((v >> 41) & 0x3fffff) == j) { hit = 1; v0 = v; }
+        }
+      }
+      hit = __builtin_amdgcn_readfirstlane(hit);
+      if (hit == 1) {  // the owner passed through this very cell: same path from here on
+        mseg = __builtin_amdgcn_readfirstlane((int)((v0 >> 30) & 0x7ff));
+        midx = __builtin_amdgcn_readfirstlane((int)(v0 & 0x3fffffff));
+        break;
+      }
+    }
     const int w = (i - 1) & (kBandRows - 1);
     const int t = w >> 3;
     {  // ---- make the tile holding the 8x8 block at (i, j) current
       const int b = (i - 1) / kBandRows;
       const int tl = t > 0 ? t - 1 : 0;  // lowest lane of this band the block touches
-      const int s = Y::step(t, w & 7, j);
+      const int s = Y::step(t, w & 7, j, Y::hb(b));
       if (b != tb || s < C::TS * tq || tl < tt0 || t >= tt0 + C::TL) {
         const int q = s / C::TS;
+        if (sc.tdone && (b >> sc.task_shift) < task_ok) {  // entering rows of a task not yet seen done
+          const int tsk = b >> sc.task_shift;
+          const unsigned long long t0w = __builtin_amdgcn_s_memrealtime();
+          while (__hip_atomic_load((gu32*)(sc.tdone + tsk), RLX_AGENT) == 0u) {
+            __builtin_amdgcn_s_sleep(8);
+            if (__builtin_amdgcn_s_memrealtime() - t0w > 400000000ull) {  // ~4 s: a fill task never finished
+              if (lane == 0) atomicOr(a.err, 32u);
+              return SegOut{Lc, i, j, -2, 0};
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          task_ok = tsk;
+        }
         drain();
         n_sw++;
         if (C::NB == 2 && b == pb && q == pq && tl >= pt0 && t < pt0 + C::TL) {
@@ -374,7 +461,7 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
         flush(Lc & ~3);  // issued after the tile landed: the stores drain during this window's walk
         tb = b;
         tq = q;
-        yw = C::ywin(q, tt0);
+        yw = C::ywin(q, tt0, Y::hb(b));
         pb = -1;
         if (C::NB == 2 && q > 0) {  // the walk moves down the band: prefetch the next window
           pt0 = max(0, t - (C::TL - 1));
@@ -390,9 +477,10 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
     const unsigned tbase = lds_addr(&L.tile[cur][0]);
     const unsigned xb = lds_addr(&L.xs[cur][0]), yb = lds_addr(&L.ys[cur][0]);
     // LDS address of staged cell (row ww of band tb, column jj) and its bit shift
+    const int hh = Y::hb(tb);
     auto taddr = [&](int ww, int jj, int& sh) -> unsigned {
-      const int tt = ww >> 3, rr = ww & 7, ss = Y::step(tt, rr, jj);
-      sh = Y::shift(ss, rr);
+      const int tt = ww >> 3, rr = ww & 7, ss = Y::step(tt, rr, jj, hh);
+      sh = Y::shift(ss, rr, hh);
       return tbase + 4u * (unsigned)(((ss / SPC - cbase) * RPC + Y::slot(rr)) * C::TL + (tt - tt0));
     };
     unsigned vx, vy, vg, vu, vd;
@@ -426,8 +514,8 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
       auto gaddr = [&](int ii, int jj, int& sh) -> unsigned {
         if (ii <= 0 || jj <= 0) { sh = 0; return ~0u; }
         const int ww = ii - 1 - tb * kBandRows;
-        const int tt = ww >> 3, rr = ww & 7, ss = Y::step(tt, rr, jj);
-        sh = Y::shift(ss, rr);
+        const int tt = ww >> 3, rr = ww & 7, ss = Y::step(tt, rr, jj, hh);
+        sh = Y::shift(ss, rr, hh);
         if (ww < 0 || tt < tt0 || tt >= tt0 + C::TL || ss < slo || ss >= shi) return ~1u;
         return taddr(ww, jj, sh);
       };
@@ -448,7 +536,7 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
           : "memory");
       const bool fx = !xin && ci >= 1, fy = !yin && cj >= 1;
       if (fx || fy || ag == ~1u || au == ~1u || ad == ~1u) {
-        const Five f = tb_fallback<W, PK>(a.mat, pd, bdw, xg, yg, ci, cj, fx, fy, ag == ~1u, au == ~1u, ad == ~1u,
+        const Five f = tb_fallback<W, LY>(a.mat, pd, bdw, xg, yg, ci, cj, fx, fy, ag == ~1u, au == ~1u, ad == ~1u,
                                           shg, shu, shd, Five{vx, vy, vg, vu, vd});
         vx = f.v[0]; vy = f.v[1]; vg = f.v[2]; vu = f.v[3]; vd = f.v[4];
       }
@@ -466,7 +554,9 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
     // reaches the border); the walk is a chain of v_readlane with a scalar
     // lane index, one byte store per step.
     const int nli = li + (isD || isU ? 1 : 0), nlj = lj + (isU ? 0 : 1);
-    const bool leaves = nli > 7 || nlj > 7 || i - nli <= 0 || j - nlj <= 0;
+    // (segments) also stop on entering a record row
+    const bool leaves = nli > 7 || nlj > 7 || i - nli <= 0 || j - nlj <= 0 ||
+                        (sc.recs && nli > li && ((i - nli) & (kRecRows - 1)) == 0);
     const unsigned code = (isD ? (unsigned)'D' : isU ? (unsigned)'U' : (unsigned)'L') |
                           ((leaves ? 64u : (unsigned)(nli * 8 + nlj)) << 8);
     unsigned long long tW = prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -493,9 +583,16 @@ __device__ __forceinline__ void trace_pair(const FillArgs& a, const PairDesc& pd
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   flush(Lc);
   drain();
+  return SegOut{Lc, i, j, mseg, midx};
+}
+
+// Whole-pair trace from (m, n) into the pair's op buffer (nw_align, nw_align_pk).
+template <int W, int LY = 0>
+__device__ __forceinline__ void trace_whole(const FillArgs& a, const PairDesc& pd, TbLds<W, LY>& L, int lane) {
+  const SegOut o = trace_pair<W, LY>(a, pd, L, lane, SegCtx{a.ops + pd.ops_off, pd.m, pd.n, 0, nullptr, nullptr, 0});
   if (lane == 0) {
-    a.oplen[pd.slot] = Lc;
-    a.endij[pd.slot] = make_int2(i, j);
+    a.oplen[pd.slot] = o.len;
+    a.endij[pd.slot] = make_int2(o.ei, o.ej);
   }
 }
 
@@ -637,7 +734,7 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
-      trace_pair<W>(a, pd, tbl[wid], lane);
+      trace_whole<W>(a, pd, tbl[wid], lane);
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
     }
   }
@@ -756,7 +853,7 @@ __global__ __launch_bounds__(256) void nw_align_pk(FillArgs a) {
   __shared__ __attribute__((aligned(16))) int ring_all[4][128];
   // SEL window per super-block: SEL[64sb-128 .. 64sb+64), two slots per wave
   __shared__ __attribute__((aligned(16))) unsigned swin_all[4][384];
-  __shared__ __attribute__((aligned(16))) TbLds<W, true> tbl[4];
+  __shared__ __attribute__((aligned(16))) TbLds<W, 1> tbl[4];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   int* ring = ring_all[wid];
@@ -882,11 +979,306 @@ __global__ __launch_bounds__(256) void nw_align_pk(FillArgs a) {
       if (a.dbg_notrace) {  // debug (NWK_NOTRACE): fill-only timing, results invalid
         if (lane == 0) { a.oplen[pd.slot] = 0; a.endij[pd.slot] = make_int2(pd.m, pd.n); }
       } else {
-        trace_pair<W, true>(a, pd, tbl[wid], lane);
+        trace_whole<W, 1>(a, pd, tbl[wid], lane);
       }
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
     }
   }
+}
+
+// ===========================================================================
+// Band-pair packed fill (kPacked2): one wave carries bands 2p (low halves)
+// and 2p+1 (high halves) of a pair as int16 pairs, the odd band 64 columns
+// behind, so lane t holds P[r] = {row r of band 2p at column s-t+1, row r of
+// band 2p+1 at column s-t-63} (layout LY 2).  Band 2p+1's first row reads
+// band 2p's last row from lane 63 one step earlier through DPP wave_ror:1;
+// lanes keep the 1-column skew of nw_align, so a band pair adds 127 steps of
+// pipeline lag (nw_align_pk: 190 per single band), the hand-off through HBM
+// happens once per 1024 rows, and the per-step overhead is shared by 16
+// cells.  Recurrence, base re-centring and 4-bit storage as nw_align_pk
+// (across one wave G spans < 2*pgap*1152 + drift: int16 for pgap <= 7).
+// ===========================================================================
+// Eight wavefront steps s0..s0+7 (s0 % 8 == 0).
+//   bslot: LDS ring of B[s0+1 .. s0+8] - base (band-above row, low 16 bits)
+//   srow:  LDS SEL64 window at this lane's column for step s0 (8 words)
+//   upsel: v_perm selector of up0: lane 0 {B, lane 63's band-2p row}, others identity
+template <bool MASK>
+__device__ __forceinline__ void step_block_pk2(int s0, int lane, unsigned (&P)[kRows], unsigned& U, unsigned& stage,
+                                               const unsigned (&pl)[kRows], const unsigned (&ph)[kRows],
+                                               const unsigned* srow, const int* bslot, unsigned upsel, unsigned* mptr,
+                                               bool pub, u64* gpub, unsigned epoch, int base) {
+  const int4 bA = *reinterpret_cast<const int4*>(bslot);
+  const int4 bB = *reinterpret_cast<const int4*>(bslot + 4);
+  const int bv[8] = {bA.x, bA.y, bA.z, bA.w, bB.x, bB.y, bB.z, bB.w};
+  unsigned sel[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sel[k] = srow[k];
+  unsigned Xa[kRows];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    // lane 63's {row 7 of band 2p, row 7 of band 2p+1} enters the publish window
+    stage = (unsigned)__builtin_amdgcn_update_dpp((int)P[kRows - 1], (int)stage, 0x130 /*wave_shl:1*/, 0xf, 0xf, false);
+    if (k == 7 && pub) st_granule(gpub, epoch, ((int)stage >> 16) + base);
+    // up of row 0: lane t-1's row 7 (both bands); lane 0: {band above, lane 63's band-2p row 7}
+    const unsigned x = (unsigned)__builtin_amdgcn_update_dpp(0, (int)P[kRows - 1], 0x13c /*wave_ror:1*/, 0xf, 0xf, false);
+    const unsigned up = __builtin_amdgcn_perm(x, (unsigned)bv[k], upsel);
+    const unsigned dg0 = U;
+    U = up;
+    unsigned sk = sel[k];
+    asm volatile("" : "+v"(sk));
+    unsigned Pn[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      const unsigned K = __builtin_amdgcn_perm(ph[r], pl[r], sk);
+      const unsigned dg = r ? P[r - 1] : dg0;
+      const unsigned ur = r ? Pn[r - 1] : up;
+      Pn[r] = pk_min(pk_min(pk_add(dg, K), P[r]), ur);
+    }
+    if constexpr (MASK) {  // columns <= 0 stay on the border (G = 0; base is 0 here)
+      const int s = s0 + k;
+      const unsigned M = s >= lane + 64 ? 0xffffffffu : (s >= lane ? 0x0000ffffu : 0u);
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) Pn[r] &= M;
+    }
+    if (k & 1) {
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) {
+        const unsigned X = __builtin_amdgcn_perm(Pn[r], P[r], 0x06040200u);
+        if ((k & 3) == 1) {
+          Xa[r] = X;
+        } else {
+          const unsigned D = (Xa[r] & 0x0f0f0f0fu) | ((X << 4) & 0xf0f0f0f0u);
+          __builtin_nontemporal_store(D, mptr + ((k >> 2) * kRows + r) * kWave);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) P[r] = Pn[r];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__device__ __forceinline__ void asm_load_S2(const unsigned* p, unsigned& a, unsigned& b) {
+  asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %2, off offset:256"
+               : "=&v"(a), "=&v"(b)
+               : "v"(p)
+               : "memory");
+}
+
+__global__ __launch_bounds__(256) void nw_align_pk2(FillArgs a) {
+  constexpr int W = 4;
+  __shared__ __attribute__((aligned(16))) int ring_all[4][128];
+  // SEL64 window per super-block: SEL64[64sb-64 .. 64sb+64), two slots per wave
+  __shared__ __attribute__((aligned(16))) unsigned swin_all[4][256];
+  __shared__ __attribute__((aligned(16))) TbLds<W, 2> tbl[4];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  int* ring = ring_all[wid];
+  unsigned* swin = swin_all[wid];
+  const unsigned upsel = lane == 0 ? 0x05040100u : 0x07060504u;
+  if (a.stamps && threadIdx.x == 0) atomicMin(a.stamps + 11 * a.ntasks_pairs, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+
+  for (;;) {
+    unsigned tk = 0;
+    if (lane == 0) tk = atomicAdd(a.counter, 1u);
+    tk = __builtin_amdgcn_readfirstlane(tk);
+    if (tk >= (unsigned)a.ntasks) return;
+    if (__hip_atomic_load((gu32*)a.err, RLX_AGENT) != 0u) return;
+    const int2 task = a.tasks[tk];
+    const PairDesc pd = a.pairs[task.x];
+    const int bp = task.y;                    // band pair: bands 2bp, 2bp+1
+    const int ntp = (pd.nbands + 1) >> 1;     // band pairs of the pair
+    const int row0 = 2 * bp * kBandRows + lane * kRows;
+    unsigned pl[kRows], ph[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      unsigned p0 = 0, p1 = 0;
+      const unsigned c0 = row0 + r < pd.m ? a.codes[pd.x_off + row0 + r] : 0u;
+      const unsigned c1 = row0 + kBandRows + r < pd.m ? a.codes[pd.x_off + row0 + kBandRows + r] : 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        p0 |= ((unsigned)(c0 == (unsigned)q ? a.K0 : a.K1) & 0xffu) << (8 * q);
+        p1 |= ((unsigned)(c1 == (unsigned)q ? a.K0 : a.K1) & 0xffu) << (8 * q);
+      }
+      pl[r] = p0;
+      ph[r] = p1;
+    }
+
+    const bool from_above = bp > 0;
+    const bool to_below = bp + 1 < ntp;
+    const int64_t bstride = (int64_t)pd.nchunks * 64;
+    const u64* gin = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)(bp > 0 ? bp - 1 : 0) * bstride + lane;
+    const int last_chunk = pd.nchunks > 0 ? pd.nchunks - 1 : 0;
+    u64* gout = a.bnd + pd.bnd_off + (int64_t)bp * bstride + lane;
+    unsigned* mptr = a.mat + pd.mat_off + (int64_t)bp * 2 * band_dwords(W, pd.sblocks) + lane;
+
+    unsigned P[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) P[r] = 0u;
+    unsigned U = 0, stage = 0;
+    int base = 0;
+    u64 pend = 0;
+    const unsigned* Sg = a.sel + pd.e_off - 64 + lane;
+    unsigned sw0, sw1;
+    asm_load_S2(Sg, sw0, sw1);
+    asm_load_granule(gin, pend);
+    wait_vm_keep<0>(sw0, sw1, pend);
+    bool ok = true;
+    constexpr int kBlockStores = 2 * kRows;
+    u64 cyc_wait = 0, cyc_wait0 = 0, n_wait = 0;
+    const u64 t_task = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+
+    for (int sb = 0; sb < pd.sblocks; ++sb) {
+      // --- band-above row for this super-block: B[64sb+1 .. 64sb+64] = chunk sb
+      int bval = 0;
+      if (from_above && sb < pd.nchunks) {
+        if (!__all((unsigned)(pend >> 32) == a.epoch)) {
+          const u64 tw = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+          pend = wait_granules(gin + 64 * sb, a.epoch, pend, a.err);
+          if (a.stamps) {
+            const u64 d = __builtin_amdgcn_s_memtime() - tw;
+            cyc_wait += d;
+            if (sb == 0) cyc_wait0 += d;
+            ++n_wait;
+          }
+          if (!__all((unsigned)(pend >> 32) == a.epoch)) { ok = false; break; }
+        }
+        bval = (int)(unsigned)pend;
+      }
+      asm_load_granule(gin + 64 * min(sb + 1, last_chunk), pend);
+      // --- re-centre the base (after the masked super-blocks 0 and 1)
+      if (sb >= 2) {
+        const int ref = (int)(short)(__builtin_amdgcn_readlane((int)P[0], 32) & 0xffff);
+        const int delta = ref & ~15;
+        const unsigned dd = ((unsigned)delta & 0xffffu) * 0x10001u;
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) P[r] = pk_sub(P[r], dd);
+        U = pk_sub(U, dd);
+        stage -= (unsigned)delta << 16;
+        base += delta;
+      }
+      int* slot = ring + (sb & 1) * 64;
+      slot[lane] = (int)((unsigned)(bval - base) & 0xffffu);
+      unsigned* w = swin + (sb & 1) * 128;
+      w[lane] = sw0;
+      w[64 + lane] = sw1;
+      asm_load_S2(Sg + 64 * (sb + 1), sw0, sw1);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+
+      const bool pub_sb = to_below && sb >= 2 && sb - 2 < pd.nchunks;
+      u64* gpub = gout + 64 * (sb >= 2 ? sb - 2 : 0);
+      for (int blk = 0; blk < 8; ++blk) {
+        const int s0 = sb * 64 + blk * 8;
+        const unsigned* srow = w + blk * 8 + 64 - lane;
+        const bool pub = pub_sb && blk == 7;
+        if (sb < 2)
+          step_block_pk2<true>(s0, lane, P, U, stage, pl, ph, srow, slot + blk * 8, upsel, mptr, pub, gpub, a.epoch,
+                               base);
+        else
+          step_block_pk2<false>(s0, lane, P, U, stage, pl, ph, srow, slot + blk * 8, upsel, mptr, pub, gpub, a.epoch,
+                                base);
+        mptr += 2 * kRows * kWave;
+        wait_vm_keep<kBlockStores>(sw0, sw1, pend);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (!ok) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.stamps && lane == 0) {
+      atomicAdd(a.stamps + 8 * pd.slot + 6, (unsigned long long)(__builtin_amdgcn_s_memtime() - t_task));
+      atomicAdd(a.stamps + 8 * pd.slot + 7, (unsigned long long)cyc_wait);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot, (unsigned long long)cyc_wait0);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 1, (unsigned long long)n_wait);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 2, (unsigned long long)pd.sblocks);
+    }
+    // --- task done (its stores were released above); the pair's last task and
+    // every spec_every-th task then trace a segment (see SegCtx)
+    if (lane == 0) __hip_atomic_store((gu32*)(a.tdone + pd.task_off + bp), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int E = pd.spec_every;
+    const bool last = bp + 1 == ntp;
+    if (last || (E > 0 && (bp + 1) % E == 0)) {
+      constexpr int RT = 2 * kBandRows;  // rows per task
+      const int k = last ? (E > 0 ? (ntp - 1) / E : 0) : (bp + 1) / E - 1;
+      const int64_t off = (int64_t)E * RT * k * (k + 1) / 2 + (int64_t)k * pd.n;
+      int i0 = pd.m, j0 = pd.n;
+      if (!last) {  // guess: the proportional diagonal
+        i0 = (bp + 1) * RT;
+        j0 = (int)(((int64_t)pd.n * i0) / pd.m);
+        j0 = j0 < 1 ? 1 : j0;
+      }
+      if (last && a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
+      SegOut o{0, i0, j0, -1, 0};
+      if (a.dbg_notrace) {
+        o = SegOut{0, pd.m, pd.n, -1, 0};
+      } else {
+        const SegCtx sc{a.segops + pd.segops_off + off, i0, j0, bp, E > 0 ? a.recs + pd.rec_off : nullptr,
+                        a.tdone + pd.task_off, 1};
+        o = trace_pair<W, 2>(a, pd, tbl[wid], lane, sc);
+      }
+      if (lane == 0) {
+        int* si = a.seginfo + 8 * (pd.task_off + bp);
+        si[0] = o.len; si[1] = o.ei; si[2] = o.ej; si[3] = o.mseg; si[4] = o.midx;
+        si[5] = (int)(off & 0x7fffffff); si[6] = (int)(off >> 31);
+      }
+      if (last && a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+}
+
+// Resolves each pair's segment chain (nw_align_pk2): from the last task's
+// segment follow the merge links, copying [from, len) of every segment on the
+// way into the pair's contiguous op buffer; the end cell comes from the
+// segment that ran to the border.  One workgroup per pair.
+__global__ __launch_bounds__(256) void nw_gather(FillArgs a, int npairs) {
+  __shared__ int pc_seg[kMaxTasksPerPair], pc_from[kMaxTasksPerPair];
+  __shared__ int n_pc, fin_i, fin_j, bad;
+  const int q = blockIdx.x;
+  if (q >= npairs) return;
+  const PairDesc pd = a.pairs[q];
+  const int ntp = (pd.nbands + 1) >> 1;
+  if (threadIdx.x == 0) {
+    int s = ntp - 1, from = 0, n = 0;
+    bad = 0;
+    for (;;) {
+      const int* si = a.seginfo + 8 * (pd.task_off + s);
+      if (n >= ntp || si[3] == -2 || from < 0 || from > si[0]) { bad = 1; break; }
+      pc_seg[n] = s;
+      pc_from[n] = from;
+      ++n;
+      if (si[3] < 0) { fin_i = si[1]; fin_j = si[2]; break; }
+      from = si[4];
+      s = si[3];
+      if (s < 0 || s >= ntp) { bad = 1; break; }
+    }
+    n_pc = n;
+  }
+  __syncthreads();
+  if (bad) {
+    if (threadIdx.x == 0) atomicOr(a.err, 64u);
+    return;
+  }
+  uint8_t* out = a.ops + pd.ops_off;
+  int pos = 0;
+  for (int c = 0; c < n_pc; ++c) {
+    const int* si = a.seginfo + 8 * (pd.task_off + pc_seg[c]);
+    const int64_t off = (int64_t)si[5] | ((int64_t)si[6] << 31);
+    const uint8_t* src = a.segops + pd.segops_off + off;
+    const int from = pc_from[c], len = si[0];
+    for (int t = from + threadIdx.x; t < len; t += blockDim.x) out[pos + t - from] = src[t];
+    pos += len - from;
+  }
+  if (threadIdx.x == 0) {
+    a.oplen[pd.slot] = pos;
+    a.endij[pd.slot] = make_int2(fin_i, fin_j);
+  }
+}
+
+hipError_t launch_gather(const FillArgs& a, int npairs, hipStream_t s) {
+  hipLaunchKernelGGL(nw_gather, dim3(npairs), dim3(256), 0, s, a, npairs);
+  return hipGetLastError();
 }
 
 // ===========================================================================
@@ -1042,7 +1434,7 @@ __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairD
         asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ad) : "memory");
         code = (v >> (4 * (ss & (SPD - 1)))) & 15u;
       } else {
-        code = getG_global<4, false>(a.mat, pd, bdw, ci, cj);
+        code = getG_global<4, 0>(a.mat, pd, bdw, ci, cj);
       }
     }
     if (prog && lane == 0) __hip_atomic_store((gu32*)prog, 0x51000000u | (code & 0xff) << 8 | (nit & 0xff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1256,6 +1648,10 @@ hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStrea
       if (bits != 4) return hipErrorInvalidValue;
       hipLaunchKernelGGL(nw_align_pk, dim3(grid), dim3(256), 0, s, a);
       return hipGetLastError();
+    case kPacked2:
+      if (bits != 4) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(nw_align_pk2, dim3(grid), dim3(256), 0, s, a);
+      return hipGetLastError();
     case kProfile: return fill_m<kProfile>(bits, a, grid, s);
     case kCompare: return fill_m<kCompare>(bits, a, grid, s);
     case kLiteral: return bits == 32 ? fill_w<kLiteral, 32>(a, grid, s) : hipErrorInvalidValue;
@@ -1273,9 +1669,11 @@ static int occ_w() {
 
 int fill_blocks_per_cu(int mode, int bits) {
   if (mode == kLiteral) return occ_w<kLiteral, 32>();
-  if (mode == kAffine || mode == kPacked) {
+  if (mode == kAffine || mode == kPacked || mode == kPacked2) {
     int n = 0;
-    const void* f = mode == kAffine ? reinterpret_cast<const void*>(&nw_align_affine) : reinterpret_cast<const void*>(&nw_align_pk);
+    const void* f = mode == kAffine   ? reinterpret_cast<const void*>(&nw_align_affine)
+                    : mode == kPacked ? reinterpret_cast<const void*>(&nw_align_pk)
+                                      : reinterpret_cast<const void*>(&nw_align_pk2);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 256, 0) != hipSuccess) return 1;
     return n > 0 ? n : 1;
   }

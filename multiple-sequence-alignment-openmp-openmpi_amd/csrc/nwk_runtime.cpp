@@ -117,6 +117,8 @@ struct PairWork {
   int i, j;         // x = seq i (rows), y = seq j (columns)
   int m, n;
   int64_t mat_dw, bnd_gr, ops_b;  // footprint
+  int64_t segops_b, segctl_b;     // kPacked2 segmented traceback: move buffers, control (flags, info, records)
+  int spec;                       // kPacked2: spec_every
 };
 
 }  // namespace
@@ -142,13 +144,14 @@ struct nwk_ctx {
   DevBuf d_codes[2];            // [0] profile codes, [1] raw bytes
   DevBuf d_E[2];
   bool built[2] = {false, false};
-  DevBuf d_sel[2];              // kPacked selector streams: [0] hi = 0x00, [1] hi = 0xff
-  bool built_sel[2] = {false, false};
+  DevBuf d_sel[4];              // selector streams: [hi 0x00, hi 0xff] x [kPacked (lag 1), kPacked2 (lag 64)]
+  bool built_sel[4] = {false, false, false, false};
 
   // batch buffers
   DevBuf d_work;                // matrices | boundary granules | op strings
   int64_t clean_b = 0;          // leading bytes of d_work holding only zeros / old-epoch granules
   DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij, d_done, d_stamps, d_prog;
+  DevBuf d_segctl;              // kPacked2: task-done flags | segment info | traceback records
   HostBuf h_tasks;
   HostBuf h_pairs[2], h_oplen[2], h_endij[2], h_ops[2];  // double-buffered: batch b+1 runs while b finalizes
 
@@ -180,6 +183,7 @@ void nwk_ctx_destroy(nwk_ctx* c) {
   c->d_work.release();
   c->d_pairs.release(); c->d_tasks.release(); c->d_ctl.release();
   c->d_oplen.release(); c->d_endij.release(); c->d_done.release(); c->d_stamps.release();
+  c->d_segctl.release(); c->d_prog.release();
   c->h_tasks.release();
   for (int b = 0; b < 2; ++b) {
     c->h_pairs[b].release(); c->h_oplen[b].release(); c->h_endij[b].release(); c->h_ops[b].release();
@@ -243,7 +247,7 @@ int nwk_set_sequences(nwk_ctx* c, const uint8_t* seqs, const int64_t* offsets, i
   for (int b = 0; b < 256; ++b)
     if (seen[b]) c->code_of[b] = (uint8_t)c->alpha++;
   c->built[0] = c->built[1] = false;
-  c->built_sel[0] = c->built_sel[1] = false;
+  for (auto& b : c->built_sel) b = false;
   // layout: codes 8-aligned; E / SEL with kEPad entries before column 0 and kETail past the end
   c->c_off.resize(k);
   c->e_off.resize(k);
@@ -303,8 +307,10 @@ int build_encoding(nwk_ctx* c, int kind) {
 // 4 + code(y[a-1]), hi} -- the v_perm selector of the substitution profile
 // bytes of a row pair at column a+1 (row q) and a (row q+4); hi = 0x0d
 // (byte 0xff: both K < 0) or 0x0c (byte 0x00: both K >= 0) sign-extends.
-int build_sel(nwk_ctx* c, int neg) {
-  if (c->built_sel[neg]) return NWK_OK;
+// kPacked2 (lag 64): SEL64[a] = {code(y[a]), hi, 4 + code(y[a-64]), hi}.
+int build_sel(nwk_ctx* c, int neg, int lag) {
+  const int idx = neg + (lag == 64 ? 2 : 0);
+  if (c->built_sel[idx]) return NWK_OK;
   const int k = c->k;
   const int64_t nE = k ? c->e_off[k - 1] + (c->off[k] - c->off[k - 1]) + kETail : 64;
   std::vector<uint32_t> S((size_t)nE, 0);
@@ -314,12 +320,12 @@ int build_sel(nwk_ctx* c, int neg) {
     const int64_t L = c->off[s + 1] - c->off[s];
     uint32_t* e = S.data() + c->e_off[s];
     auto code = [&](int64_t t) -> uint32_t { return t >= 0 && t < L ? c->code_of[y[t]] : 0u; };
-    for (int64_t a = -kEPad; a < L + kETail; ++a) e[a] = code(a) | hi << 8 | (4u + code(a - 1)) << 16 | hi << 24;
+    for (int64_t a = -kEPad; a < L + kETail; ++a) e[a] = code(a) | hi << 8 | (4u + code(a - lag)) << 16 | hi << 24;
   }
   int rc;
-  if ((rc = c->d_sel[neg].ensure(S.size() * 4)) != NWK_OK) return rc;
-  HIP_TRY(hipMemcpy(c->d_sel[neg].p, S.data(), S.size() * 4, hipMemcpyHostToDevice));
-  c->built_sel[neg] = true;
+  if ((rc = c->d_sel[idx].ensure(S.size() * 4)) != NWK_OK) return rc;
+  HIP_TRY(hipMemcpy(c->d_sel[idx].p, S.data(), S.size() * 4, hipMemcpyHostToDevice));
+  c->built_sel[idx] = true;
   return NWK_OK;
 }
 
@@ -363,20 +369,40 @@ int choose_plan(const nwk_ctx* c, const Scoring& sc, Plan* pl) {
   pl->K1 = (int)((int64_t)pxy - 2 * (int64_t)pgap);
   // two cells per register when the profile bytes sign-extend uniformly
   // (K0, K1 both < 0 or both >= 0); NWK_PACKED=0 keeps nw_align (A/B)
-  static const bool packed_off = getenv("NWK_PACKED") && atoi(getenv("NWK_PACKED")) == 0;
-  if (pl->mode == kProfile && pl->bits == 4 && !packed_off && ((pl->K0 < 0) == (pl->K1 < 0))) pl->mode = kPacked;
+  // NWK_PACKED=0 / 1 select nw_align / nw_align_pk instead of the default nw_align_pk2 (A/B)
+  static const int packed = getenv("NWK_PACKED") ? atoi(getenv("NWK_PACKED")) : 2;
+  if (pl->mode == kProfile && pl->bits == 4 && packed > 0 && ((pl->K0 < 0) == (pl->K1 < 0)))
+    pl->mode = packed == 1 ? kPacked : kPacked2;
   return NWK_OK;
 }
 
 // 64-step super-blocks per band: the last band-row value of column n leaves
 // lane 63 at step n + 62 (nw_align) or n + 126 (nw_align_pk, 2-column skew).
-inline int sblocks_of(int mode, int64_t nch) { return (int)(nch + (mode == kPacked ? 2 : 1)); }
+inline int sblocks_of(int mode, int64_t nch) { return (int)(nch + (mode == kPacked || mode == kPacked2 ? 2 : 1)); }
+// Fill tasks per pair: bands, or band pairs (kPacked2).
+inline int64_t tasks_of(int mode, int64_t nb) { return mode == kPacked2 ? (nb + 1) / 2 : nb; }
+
+// kPacked2 segmented traceback footprint for a speculative segment every E
+// tasks (E = 0: one whole-pair segment): move buffers (segment k starts on
+// row (k+1)*E*RT and may run to the border: capacity row + n) and control.
+void seg_footprint(PairWork* w, int E) {
+  const int64_t RT = 2 * kBandRows, nt = ceil_div(w->m, RT);
+  if (nt > kMaxTasksPerPair || w->n >= (1 << 22)) E = 0;  // record fields: 11-bit segment, 22-bit column
+  const int64_t K = E > 0 ? (nt - 1) / E : 0;
+  w->spec = E;
+  w->segops_b = round_up((int64_t)E * RT * K * (K + 1) / 2 + K * (int64_t)w->n + w->m + w->n, 16);
+  w->segctl_b = nt * (4 + 32) + (w->m / 128 + 1) * 16;
+}
 
 void footprint(PairWork* w, int bits, int mode, bool affine) {
   const int64_t nb = ceil_div(w->m, kBandRows);
   const int64_t nch = ceil_div(w->n, 64);
-  w->mat_dw = nb * band_dwords(bits, sblocks_of(mode, nch));
-  w->bnd_gr = (nb - 1) * nch * 64 * (affine ? 2 : 1);  // affine: H and F boundary rows
+  const int64_t nt = tasks_of(mode, nb);
+  w->segops_b = w->segctl_b = 0;
+  w->spec = 0;
+  if (mode == kPacked2) seg_footprint(w, 0);
+  w->mat_dw = (mode == kPacked2 ? 2 * nt : nb) * band_dwords(bits, sblocks_of(mode, nch));
+  w->bnd_gr = (nt - 1) * nch * 64 * (affine ? 2 : 1);  // affine: H and F boundary rows
   w->ops_b = round_up((int64_t)w->m + w->n, 16);
 }
 
@@ -521,17 +547,44 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   }
   if (!dp.empty()) {
     if ((rc = build_encoding(c, pl.kind)) != NWK_OK) return rc;
-    if (pl.mode == kPacked && (rc = build_sel(c, pl.K0 < 0 ? 1 : 0)) != NWK_OK) return rc;
+    if ((pl.mode == kPacked || pl.mode == kPacked2) &&
+        (rc = build_sel(c, pl.K0 < 0 ? 1 : 0, pl.mode == kPacked2 ? 64 : 1)) != NWK_OK)
+      return rc;
   }
   // Largest first (LPT inside the device; longest bands dequeued first).
-  std::sort(dp.begin(), dp.end(), [](const PairWork& a, const PairWork& b) {
+  // kPacked2 (NWK_SORT != 0): by traceback length m + n first, so the pairs
+  // filled last -- whose traces form the kernel's tail -- are the shortest to trace.
+  // NWK_SORT: 1 = m + n, 2 = max(m, n) (wide pairs merge their segments slowest), 0 = cells only
+  static const int sort_trace = getenv("NWK_SORT") ? atoi(getenv("NWK_SORT")) : 2;
+  const int by_trace = pl.mode == kPacked2 ? sort_trace : 0;
+  std::sort(dp.begin(), dp.end(), [by_trace](const PairWork& a, const PairWork& b) {
+    const int ka = by_trace == 1 ? a.m + a.n : std::max(a.m, a.n), kb = by_trace == 1 ? b.m + b.n : std::max(b.m, b.n);
+    if (by_trace && ka != kb) return ka > kb;
     const double ca = (double)a.m * a.n, cb = (double)b.m * b.n;
     if (ca != cb) return ca > cb;
     return a.id < b.id;
   });
+  // Segmented traceback (kPacked2): only the pairs dequeued last -- the last
+  // NWK_SPEC_FRAC (default 0.35) of the cells -- trace speculatively (a
+  // segment every NWK_SPEC tasks, default 2); earlier pairs' whole-pair
+  // traces overlap the remaining fill anyway.
+  if (pl.mode == kPacked2) {
+    static const int spec_env = getenv("NWK_SPEC") ? atoi(getenv("NWK_SPEC")) : 2;
+    static const double frac = getenv("NWK_SPEC_FRAC") ? atof(getenv("NWK_SPEC_FRAC")) : 0.35;
+    double tot = 0, acc = 0;
+    for (const auto& w : dp) tot += (double)w.m * w.n;
+    for (auto& w : dp) {
+      seg_footprint(&w, acc >= (1.0 - frac) * tot ? std::max(0, spec_env) : 0);
+      acc += (double)w.m * w.n;
+    }
+  }
   int bpc = fill_blocks_per_cu(pl.mode, pl.bits);
-  static const int bpc_cap = getenv("NWK_BPC") ? atoi(getenv("NWK_BPC")) : 0;  // experiment: waves per SIMD
-  if (bpc_cap > 0 && bpc_cap < bpc) bpc = bpc_cap;
+  // waves per SIMD: nw_align_pk2 measured best at 2 (band chains run at the
+  // pace of their slowest member; more waves per SIMD only add waiting);
+  // NWK_BPC overrides (experiments)
+  if (pl.mode == kPacked2) bpc = std::min(bpc, 2);
+  static const int bpc_cap = getenv("NWK_BPC") ? atoi(getenv("NWK_BPC")) : 0;
+  if (bpc_cap > 0) bpc = std::min(bpc_cap, fill_blocks_per_cu(pl.mode, pl.bits));
   const int grid = bpc * c->cus;
   float ms = 0;
 
@@ -546,15 +599,15 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   while (pos < dp.size()) {
     // ---- form a batch that fits the HBM budget
     size_t end = pos;
-    int64_t mat = 0, bnd = 0, ops = 0;
+    int64_t mat = 0, bnd = 0, ops = 0, segops = 0;
     while (end < dp.size()) {
       const PairWork& w = dp[end];
-      const int64_t need = (mat + w.mat_dw) * 4 + (bnd + w.bnd_gr) * 8 + ops + w.ops_b + 4096;
+      const int64_t need = (mat + w.mat_dw) * 4 + (bnd + w.bnd_gr) * 8 + ops + w.ops_b + segops + w.segops_b + 4096;
       if (need > c->budget && end > pos) break;
       if (need > c->budget)
         return fail(NWK_ENOMEM, "pair %lld (%d x %d) needs %lld bytes > HBM budget %lld", (long long)w.id,
                     w.m, w.n, (long long)need, (long long)c->budget);
-      mat += w.mat_dw; bnd += w.bnd_gr; ops += w.ops_b;
+      mat += w.mat_dw; bnd += w.bnd_gr; ops += w.ops_b; segops += w.segops_b;
       ++end;
     }
     const int np = (int)(end - pos);
@@ -566,7 +619,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     const int64_t bnd_need_b = bnd * 8 + 4096;  // + slack: band 0's dummy prefetches
     const int64_t mat_base_b = round_up(bnd_need_b, 256);
     const int64_t ops_base_b = round_up(mat_base_b + mat * 4, 256);
-    const int64_t work_b = ops_base_b + ops + 256;  // + slack: traceback tile overrun of the last band
+    const int64_t segops_base_b = round_up(ops_base_b + ops, 256);
+    const int64_t work_b = segops_base_b + segops + 256;  // + slack: traceback tile overrun of the last band
     void* const old_work = c->d_work.p;
     if ((rc = c->d_work.ensure((size_t)work_b)) != NWK_OK) return rc;
     if (c->d_work.p != old_work) c->clean_b = 0;
@@ -578,7 +632,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     const int par = st.batches & 1;  // host buffer set of this batch
     if ((rc = c->h_pairs[par].ensure(sizeof(PairDesc) * np)) != NWK_OK) return rc;
     PairDesc* pd = c->h_pairs[par].as<PairDesc>();
-    int64_t mo = 0, bo = 0, oo = 0, ntasks = 0;
+    int64_t mo = 0, bo = 0, oo = 0, ntasks = 0, so = 0, ro = 0;
     int maxb = 0;
     for (int q = 0; q < np; ++q) {
       const PairWork& w = dp[pos + q];
@@ -595,9 +649,15 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       d.nchunks = (int)ceil_div(w.n, 64);
       d.sblocks = sblocks_of(pl.mode, d.nchunks);
       d.slot = q;
+      d.spec_every = w.spec;
+      d.task_off = ntasks;  // one tdone / seginfo entry per task
+      d.rec_off = ro;
+      d.segops_off = so;
+      ro += 2 * (w.m / 128 + 1);
+      so += w.segops_b;
       mo += w.mat_dw; bo += w.bnd_gr; oo += w.ops_b;
-      ntasks += d.nbands;
-      maxb = std::max(maxb, d.nbands);
+      ntasks += tasks_of(pl.mode, d.nbands);
+      maxb = std::max(maxb, (int)tasks_of(pl.mode, d.nbands));
     }
     if ((rc = c->h_tasks.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
     int2* tk = c->h_tasks.as<int2>();
@@ -609,19 +669,19 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     if (order == 1) {  // band-major (experiment)
       for (int b = 0; b < maxb; ++b)
         for (int q = 0; q < np; ++q)
-          if (b < pd[q].nbands) tk[t++] = make_int2(q, b);
+          if (b < tasks_of(pl.mode, pd[q].nbands)) tk[t++] = make_int2(q, b);
     } else if (order >= 2) {  // groups of `order` pairs, band-major inside a group (experiment)
       for (int g0 = 0; g0 < np; g0 += order) {
         const int g1 = std::min(np, g0 + order);
         int mb = 0;
-        for (int q = g0; q < g1; ++q) mb = std::max(mb, pd[q].nbands);
+        for (int q = g0; q < g1; ++q) mb = std::max(mb, (int)tasks_of(pl.mode, pd[q].nbands));
         for (int b = 0; b < mb; ++b)
           for (int q = g0; q < g1; ++q)
-            if (b < pd[q].nbands) tk[t++] = make_int2(q, b);
+            if (b < tasks_of(pl.mode, pd[q].nbands)) tk[t++] = make_int2(q, b);
       }
     } else {
       for (int q = 0; q < np; ++q)
-        for (int b = 0; b < pd[q].nbands; ++b) tk[t++] = make_int2(q, b);
+        for (int b = 0; b < tasks_of(pl.mode, pd[q].nbands); ++b) tk[t++] = make_int2(q, b);
     }
     if ((rc = c->d_pairs.ensure(sizeof(PairDesc) * np)) != NWK_OK) return rc;
     if ((rc = c->d_tasks.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
@@ -635,6 +695,12 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipMemcpyAsync(c->d_tasks.p, tk, sizeof(int2) * ntasks, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(c->d_ctl.p, 0, 256, c->stream));
     HIP_TRY(hipMemsetAsync(c->d_done.p, 0, sizeof(unsigned) * np, c->stream));
+    const int64_t rec_base_b = round_up(ntasks * (4 + 32), 8);  // [tdone u32 | seginfo 8 x int | recs u64]
+    const int64_t segctl_b = rec_base_b + ro * 8;
+    if (pl.mode == kPacked2) {
+      if ((rc = c->d_segctl.ensure((size_t)segctl_b)) != NWK_OK) return rc;
+      HIP_TRY(hipMemsetAsync(c->d_segctl.p, 0, (size_t)segctl_b, c->stream));
+    }
 
     FillArgs fa;
     fa.pairs = c->d_pairs.as<PairDesc>();
@@ -642,7 +708,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.ntasks = (int)ntasks;
     fa.codes = c->d_codes[pl.kind].as<uint8_t>();
     fa.E = c->d_E[pl.kind].as<uint32_t>();
-    fa.sel = pl.mode == kPacked ? c->d_sel[pl.K0 < 0 ? 1 : 0].as<uint32_t>() : nullptr;
+    fa.sel = pl.mode == kPacked    ? c->d_sel[pl.K0 < 0 ? 1 : 0].as<uint32_t>()
+             : pl.mode == kPacked2 ? c->d_sel[2 + (pl.K0 < 0 ? 1 : 0)].as<uint32_t>()
+                                   : nullptr;
     fa.mat = c->d_work.as<uint32_t>();
     fa.bnd = c->d_work.as<unsigned long long>();
     fa.counter = c->d_ctl.as<unsigned>();
@@ -664,11 +732,16 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.stamps = nullptr;
     fa.ntasks_pairs = np;
     if (c->opts.verbose >= 2) {
-      if ((rc = c->d_stamps.ensure(88 * (size_t)np)) != NWK_OK) return rc;
+      if ((rc = c->d_stamps.ensure(88 * (size_t)np + 16)) != NWK_OK) return rc;
       HIP_TRY(hipMemsetAsync(c->d_stamps.p, 0, 88 * (size_t)np, c->stream));
+      HIP_TRY(hipMemsetAsync(c->d_stamps.as<uint8_t>() + 88 * (size_t)np, 0xff, 8, c->stream));  // kernel start: atomicMin
       fa.stamps = c->d_stamps.as<unsigned long long>();
     }
     fa.ops = c->d_work.as<uint8_t>();
+    fa.tdone = pl.mode == kPacked2 ? c->d_segctl.as<unsigned>() : nullptr;
+    fa.seginfo = pl.mode == kPacked2 ? reinterpret_cast<int*>(c->d_segctl.as<uint8_t>() + ntasks * 4) : nullptr;
+    fa.recs = pl.mode == kPacked2 ? reinterpret_cast<unsigned long long*>(c->d_segctl.as<uint8_t>() + rec_base_b) : nullptr;
+    fa.segops = c->d_work.as<uint8_t>() + segops_base_b;
     fa.oplen = c->d_oplen.as<int>();
     fa.endij = c->d_endij.as<int2>();
     // One persistent launch: fill bands, and each pair's traceback runs on
@@ -681,6 +754,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     }
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(launch_fill(pl.mode, pl.bits, fa, std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
+    if (pl.mode == kPacked2) HIP_TRY(launch_gather(fa, np, c->stream));  // segment chains -> op strings
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     if (c->opts.verbose >= 3) {
       fprintf(stderr, "nwk batch %d: launched mode %d bits %d grid %d, waiting\n", st.batches, pl.mode, pl.bits, grid);
@@ -726,10 +800,13 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     st.fill_ms += ms;  // fill + fused traceback (one launch)
     if (fa.stamps) {  // per-pair timeline (100 MHz ticks), relative to the earliest fill-done
-      std::vector<unsigned long long> sp(11 * (size_t)np);
-      HIP_TRY(hipMemcpy(sp.data(), fa.stamps, 88 * (size_t)np, hipMemcpyDeviceToHost));
-      unsigned long long t0 = ~0ull;
-      for (int q = 0; q < np; ++q) t0 = std::min(t0, sp[8 * q]);
+      std::vector<unsigned long long> sp(11 * (size_t)np + 1);
+      HIP_TRY(hipMemcpy(sp.data(), fa.stamps, 88 * (size_t)np + 8, hipMemcpyDeviceToHost));
+      unsigned long long t0 = ~0ull, tlast = 0;
+      for (int q = 0; q < np; ++q) t0 = std::min(t0, sp[8 * q]), tlast = std::max(tlast, sp[8 * q]);
+      const unsigned long long tk0 = sp[11 * (size_t)np];
+      fprintf(stderr, "nwk timeline: first pair filled %.3f ms, last pair filled %.3f ms after the kernel's first dequeue\n",
+              (t0 - tk0) / 1e5, (tlast - tk0) / 1e5);
       fprintf(stderr, "nwk timeline (ms after first pair filled; kernel %.3f ms): pair m x n: filled -> traced | "
                       "trace cycles switch/blocks, blocks, switches/walk-cycles | fill band-cycles, %% waiting on band above\n", ms);
       double bc = 0, wc = 0;
@@ -740,6 +817,23 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         fprintf(stderr, "  %3d %6d x %6d: %8.3f -> %8.3f (trace %.3f) | %.3g %.3g %llu %llu/%llu | %.3g %.1f%%\n", q,
                 pd[q].m, pd[q].n, (x[0] - t0) / 1e5, (x[1] - t0) / 1e5, (x[1] - x[0]) / 1e5, (double)x[2], (double)x[3],
                 x[4], x[5] >> 32, x[5] & 0xffffffffull, (double)x[6], x[6] ? 100.0 * (double)x[7] / (double)x[6] : 0.0);
+      }
+      if (pl.mode == kPacked2 && getenv("NWK_SEGDUMP")) {  // segment outcomes of the pairs traced last
+        std::vector<int> si((size_t)ntasks * 8);
+        HIP_TRY(hipMemcpy(si.data(), fa.seginfo, si.size() * 4, hipMemcpyDeviceToHost));
+        std::vector<int> ord(np);
+        for (int q = 0; q < np; ++q) ord[q] = q;
+        std::sort(ord.begin(), ord.end(), [&](int x, int y) { return sp[8 * x + 1] > sp[8 * y + 1]; });
+        for (int z = 0; z < std::min(np, 4); ++z) {
+          const int q = ord[z];
+          const int nt = (int)tasks_of(pl.mode, pd[q].nbands);
+          fprintf(stderr, "segments of pair %d (%d x %d, spec every %d):", q, pd[q].m, pd[q].n, pd[q].spec_every);
+          for (int b = 0; b < nt; ++b) {
+            const int* x = &si[8 * ((size_t)pd[q].task_off + b)];
+            if (x[0] || b == nt - 1) fprintf(stderr, " [t%d len %d end (%d,%d) -> %d@%d]", b, x[0], x[1], x[2], x[3], x[4]);
+          }
+          fprintf(stderr, "\n");
+        }
       }
       double w0 = 0, nw = 0, nsb = 0;
       for (int q = 0; q < np; ++q) {

@@ -23,7 +23,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libnwk.so")
 
 NWK_OK = 0
 ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "EKERNEL", -5: "ECOMM"}
-MODES = {0: "profile", 1: "compare", 2: "literal", 3: "affine", 4: "packed-profile"}
+MODES = {0: "profile", 1: "compare", 2: "literal", 3: "affine", 4: "packed-profile", 5: "packed-band-pairs"}
 
 
 class NwkError(RuntimeError):
