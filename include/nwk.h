@@ -57,12 +57,13 @@ typedef struct nwk_opts {
   int32_t host_threads;      /* SHA-512 / finalize threads; 0 = min(16, cores) */
   int64_t workspace_bytes;   /* HBM budget per device; 0 = 92% of free memory */
   int32_t verbose;           /* 1 = per-call statistics on stderr */
-  int32_t reserved[5];
+  int32_t finalize;          /* pair finalize (rows, penalty, SHA-512): 0 auto, 1 host, 2 device (nw_hash) */
+  int32_t reserved[4];
 } nwk_opts;
 
 typedef struct nwk_stats {
-  double fill_ms;            /* device time of the fill kernels (HIP events) */
-  double traceback_ms;       /* device time of the traceback kernels */
+  double fill_ms;            /* device time of the fill kernels incl. their fused traceback (HIP events) */
+  double traceback_ms;       /* device time after the fill launches: segment gather + device finalize */
   double total_ms;           /* wall time of the call */
   double cells;              /* sum of m*n over the pairs of the call */
   int64_t matrix_bytes;      /* HBM bytes of the stored DP matrices */
@@ -70,7 +71,8 @@ typedef struct nwk_stats {
   int32_t bits;              /* storage width used */
   int32_t mode;              /* 0 = profile, 1 = compare, 2 = literal, 3 = affine, 4 = packed profile, 5 = packed band pairs */
   int32_t fill_launches;     /* fill-kernel launches in the call */
-  int32_t reserved[4];
+  int32_t device_finalized;  /* batches whose pairs were finalized on the device */
+  int32_t reserved[3];
 } nwk_stats;
 
 /* Defaults for nwk_opts (device 0, auto everything). */

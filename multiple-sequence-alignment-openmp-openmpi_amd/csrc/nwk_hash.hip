@@ -1,0 +1,239 @@
+// nwk_hash.hip -- device-side pair finalize: alignment rows, penalty and
+// problemhash.
+//
+// Reference (skel = testing3/seqalign-mpi-skeleton.cpp):
+//   prefix fill skel:263-272, trim skel:135-154, strings skel:146-154,
+//   problemhash = sha512hex(sha512hex(align1) ++ sha512hex(align2)) skel:155-157,
+//   sha512 = sw::sha512::calculate (sha512.hh:159-164, FIPS 180-4).
+//
+// nw_rows materialises align1 / align2 of every pair in HBM (coalesced,
+// scan-based, one workgroup per pair) and sums the path cost (= dp[m][n], the
+// reference's penalty); nw_hash then runs one lane per row over 16-byte loads
+// (SHA-512 is sequential within a message), and the two digests meet through
+// a lane shuffle so the even lane can hash their 256 hex characters.  Valid when no input byte is
+// '_' (then no column is '_' in both rows and the trim keeps everything; the
+// host checks and otherwise finalizes on the CPU).
+#include "nwk_internal.h"
+
+namespace nwk {
+
+namespace {
+
+__constant__ uint64_t kK512[80] = {
+    0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+    0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+    0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+    0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+    0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+    0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+    0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+    0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+    0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+    0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+    0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+    0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+    0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+    0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+    0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+    0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+    0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+    0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+    0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+    0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+__device__ __forceinline__ uint64_t rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+struct Sha {
+  uint64_t s[8];
+  __device__ void init() {
+    s[0] = 0x6a09e667f3bcc908ULL; s[1] = 0xbb67ae8584caa73bULL; s[2] = 0x3c6ef372fe94f82bULL;
+    s[3] = 0xa54ff53a5f1d36f1ULL; s[4] = 0x510e527fade682d1ULL; s[5] = 0x9b05688c2b3e6c1fULL;
+    s[6] = 0x1f83d9abfb41bd6bULL; s[7] = 0x5be0cd19137e2179ULL;
+  }
+  // FIPS 180-4 6.4.2 on one 1024-bit block (big-endian words), rolling schedule
+  __device__ void block(uint64_t (&w)[16]) {
+    uint64_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll
+    for (int t = 0; t < 80; ++t) {
+      uint64_t wt;
+      if (t < 16) {
+        wt = w[t];
+      } else {
+        const uint64_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+        const uint64_t s0 = rotr(w15, 1) ^ rotr(w15, 8) ^ (w15 >> 7);
+        const uint64_t s1 = rotr(w2, 19) ^ rotr(w2, 61) ^ (w2 >> 6);
+        wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+        w[t & 15] = wt;
+      }
+      const uint64_t t1 = h + (rotr(e, 14) ^ rotr(e, 18) ^ rotr(e, 41)) + ((e & f) ^ (~e & g)) + kK512[t] + wt;
+      const uint64_t t2 = (rotr(a, 28) ^ rotr(a, 34) ^ rotr(a, 39)) + ((a & b) ^ (a & c) ^ (b & c));
+      h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
+  }
+};
+
+__device__ __forceinline__ uint64_t hex16(uint32_t v) {  // 8 nibbles of v -> 8 ASCII bytes, big-endian word
+  uint64_t o = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const unsigned nib = (v >> (28 - 4 * k)) & 15u;
+    o = (o << 8) | (nib < 10 ? '0' + nib : 'a' + nib - 10);
+  }
+  return o;
+}
+
+}  // namespace
+
+// Rows + penalty, one workgroup per pair: the moves are split into 256
+// contiguous chunks, a block scan gives each chunk its first x / y index, and
+// every thread writes its chunk of align1 / align2 (skel:263-272 prefix, then
+// the traced moves in forward order).
+__global__ __launch_bounds__(256) void nw_rows(HashArgs h) {
+  __shared__ int sx[256], sy[256];
+  __shared__ long long sp[256];
+  const int q = blockIdx.x;
+  const PairDesc pd = h.pairs[q];
+  const int nops = h.oplen[pd.slot];
+  const int2 e = h.endij[pd.slot];
+  const int pre = e.x > 0 ? e.x : e.y;
+  const uint8_t* ops = h.ops + pd.ops_off;
+  const uint8_t* x = h.raw + pd.x_off;
+  const uint8_t* y = h.raw + pd.y_off;
+  uint8_t* r1 = h.rows1 + (pd.ops_off - h.ops_base);
+  uint8_t* r2 = h.rows2 + (pd.ops_off - h.ops_base);
+  const int tid = threadIdx.x;
+  for (int t = tid; t < pre; t += 256) {  // prefix run
+    r1[t] = e.x > 0 ? x[t] : (uint8_t)'_';
+    r2[t] = e.x > 0 ? (uint8_t)'_' : y[t];
+  }
+  const int C = (nops + 255) / 256;
+  const int f0 = min(nops, tid * C), f1 = min(nops, f0 + C);  // forward move index f: op = ops[nops-1-f]
+  int dx = 0, dy = 0;
+  for (int f = f0; f < f1; ++f) {
+    const unsigned op = ops[nops - 1 - f];
+    const bool d = op == 'D', up = op == 'U' || op == 'u';
+    dx += (d || up) ? 1 : 0;
+    dy += (d || !up) ? 1 : 0;
+  }
+  sx[tid] = dx;
+  sy[tid] = dy;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // inclusive scan
+    const int vx = tid >= o ? sx[tid - o] : 0, vy = tid >= o ? sy[tid - o] : 0;
+    __syncthreads();
+    sx[tid] += vx;
+    sy[tid] += vy;
+    __syncthreads();
+  }
+  int ix = e.x + sx[tid] - dx, iy = e.y + sy[tid] - dy;
+  long long pen = 0;
+  for (int f = f0; f < f1; ++f) {
+    const unsigned op = ops[nops - 1 - f];
+    const bool d = op == 'D', up = op == 'U' || op == 'u';
+    const unsigned cx = (d || up) ? x[ix] : (unsigned)'_';
+    const unsigned cy = (d || !up) ? y[iy] : (unsigned)'_';
+    r1[pre + f] = (uint8_t)cx;
+    r2[pre + f] = (uint8_t)cy;
+    pen += d ? (cx == cy ? 0 : h.pxy) : (op == 'u' || op == 'l' ? h.gopen : h.gext);
+    ix += (d || up) ? 1 : 0;
+    iy += (d || !up) ? 1 : 0;
+  }
+  sp[tid] = pen;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) sp[tid] += sp[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) h.penalties[pd.slot] = (int)(sp[0] + (pre > 0 ? h.gopen + (long long)(pre - 1) * h.gext : 0));
+}
+
+// SHA-512 of one materialised row per lane (lane 2q: align1 of pair q, lane
+// 2q+1: align2), 128-byte blocks by 16-byte loads with the next block in
+// flight behind this block's rounds; then the even lane hashes the two
+// digests' hex (skel:155-157).
+__global__ __launch_bounds__(256) void nw_hash(HashArgs h) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = tid >> 1, side = tid & 1;
+  const bool live = q < h.npairs;
+  const PairDesc pd = h.pairs[live ? q : 0];
+  const int nops = live ? h.oplen[pd.slot] : 0;
+  const int2 e = live ? h.endij[pd.slot] : make_int2(0, 0);
+  const int64_t L = live ? (int64_t)(e.x > 0 ? e.x : e.y) + nops : 0;
+  const uint4* row = reinterpret_cast<const uint4*>((side ? h.rows2 : h.rows1) + (pd.ops_off - h.ops_base));
+  Sha sh;
+  sh.init();
+  const int64_t nblk = (L + 17 + 127) / 128;
+  int64_t wblk = nblk;  // per wave: as many blocks as its longest row
+  for (int o = 32; o > 0; o >>= 1) wblk = max(wblk, (int64_t)__shfl_xor(wblk, o));
+  const int64_t ndata = (L + 127) / 128;  // blocks holding message bytes (readable: row buffers are padded)
+  uint4 cur[8], nxt[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) cur[k] = ndata > 0 ? row[k] : make_uint4(0, 0, 0, 0);
+  for (int64_t bk = 0; bk < wblk; ++bk) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) nxt[k] = bk + 1 < ndata ? row[8 * (bk + 1) + k] : make_uint4(0, 0, 0, 0);
+    uint64_t w[16];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // little-endian dwords -> big-endian 64-bit words
+      w[2 * k] = ((uint64_t)__builtin_bswap32(cur[k].x) << 32) | __builtin_bswap32(cur[k].y);
+      w[2 * k + 1] = ((uint64_t)__builtin_bswap32(cur[k].z) << 32) | __builtin_bswap32(cur[k].w);
+    }
+    const int64_t b0 = 128 * bk;  // message bytes [b0, b0+128)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {  // clear bytes past L, place the 0x80 terminator
+      const int64_t s0 = b0 + 8 * k;
+      if (s0 + 8 > L) {
+        const int keep = (int)max((int64_t)0, min((int64_t)8, L - s0));
+        uint64_t v = keep > 0 ? w[k] & (~0ull << (64 - 8 * keep)) : 0ull;
+        if (L >= s0 && L < s0 + 8) v |= 0x80ull << (56 - 8 * (L - s0));
+        w[k] = v;
+      }
+    }
+    if (bk == nblk - 1) w[15] = (uint64_t)L * 8u;
+    if (bk < nblk) sh.block(w);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
+  }
+  uint64_t other[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) other[k] = __shfl_xor(sh.s[k], 1);
+  if (!live || side != 0) return;
+  Sha p;
+  p.init();
+  uint64_t w[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    w[2 * k] = hex16((uint32_t)(sh.s[k] >> 32));
+    w[2 * k + 1] = hex16((uint32_t)sh.s[k]);
+  }
+  p.block(w);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    w[2 * k] = hex16((uint32_t)(other[k] >> 32));
+    w[2 * k + 1] = hex16((uint32_t)other[k]);
+  }
+  p.block(w);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = 0;
+  w[0] = 0x8000000000000000ULL;
+  w[15] = 256 * 8;
+  p.block(w);
+  uint8_t* out = h.hashes + 64 * (int64_t)pd.slot;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint64_t v = p.s[k];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) out[8 * k + b] = (uint8_t)(v >> (56 - 8 * b));
+  }
+}
+
+hipError_t launch_hash(const HashArgs& h, hipStream_t s) {
+  if (h.npairs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(nw_rows, dim3(h.npairs), dim3(256), 0, s, h);
+  const int threads = 2 * h.npairs;
+  hipLaunchKernelGGL(nw_hash, dim3((threads + 255) / 256), dim3(256), 0, s, h);
+  return hipGetLastError();
+}
+
+}  // namespace nwk

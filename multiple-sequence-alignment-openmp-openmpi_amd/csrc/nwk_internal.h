@@ -77,6 +77,23 @@ struct FillArgs {
 
 constexpr int kMaxTasksPerPair = 2048;  // kPacked2 segment ids are 11 bits (m <= 2^21 rows)
 
+// Device pair finalize (nwk_hash.hip): rows, penalty, problemhash per pair.
+struct HashArgs {
+  const PairDesc* pairs;
+  int npairs;
+  const uint8_t* raw;      // raw sequence bytes (codes layout)
+  const uint8_t* ops;      // traced moves per pair (reversed), at pairs[].ops_off
+  int64_t ops_base;        // byte offset of the op region: pair rows sit at rows1/2 + (ops_off - ops_base)
+  uint8_t* rows1;          // align1 rows (16-aligned per pair, op-region layout, + 256 B slack)
+  uint8_t* rows2;          // align2 rows
+  const int* oplen;        // per slot
+  const int2* endij;       // per slot
+  int pxy, gopen, gext;    // move costs (linear: gopen = gext = pgap)
+  int* penalties;          // per slot
+  uint8_t* hashes;         // per slot, 64 raw bytes
+};
+hipError_t launch_hash(const HashArgs& h, hipStream_t s);
+
 // Launchers (nwk_kernels.hip).  bits in {4, 8, 16, 32}.
 hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStream_t s);
 hipError_t launch_gather(const FillArgs& a, int npairs, hipStream_t s);

@@ -152,6 +152,9 @@ struct nwk_ctx {
   int64_t clean_b = 0;          // leading bytes of d_work holding only zeros / old-epoch granules
   DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij, d_done, d_stamps, d_prog;
   DevBuf d_segctl;              // kPacked2: task-done flags | segment info | traceback records
+  DevBuf d_pen, d_hash;         // device finalize (nw_hash): per pair penalty, problemhash
+  HostBuf h_pen[2], h_hash[2];
+  bool has_us = false;          // some input byte is '_': trims need the host finalize
   HostBuf h_tasks;
   HostBuf h_pairs[2], h_oplen[2], h_endij[2], h_ops[2];  // double-buffered: batch b+1 runs while b finalizes
 
@@ -183,7 +186,8 @@ void nwk_ctx_destroy(nwk_ctx* c) {
   c->d_work.release();
   c->d_pairs.release(); c->d_tasks.release(); c->d_ctl.release();
   c->d_oplen.release(); c->d_endij.release(); c->d_done.release(); c->d_stamps.release();
-  c->d_segctl.release(); c->d_prog.release();
+  c->d_segctl.release(); c->d_prog.release(); c->d_pen.release(); c->d_hash.release();
+  for (int b = 0; b < 2; ++b) { c->h_pen[b].release(); c->h_hash[b].release(); }
   c->h_tasks.release();
   for (int b = 0; b < 2; ++b) {
     c->h_pairs[b].release(); c->h_oplen[b].release(); c->h_endij[b].release(); c->h_ops[b].release();
@@ -202,6 +206,7 @@ int nwk_ctx_create(const nwk_opts* opts, nwk_ctx** out) {
   if (opts) o = *opts;
   if (ndev <= 0) return fail(NWK_EDEVICE, "nwk_ctx_create: no HIP device visible");
   if (o.device < 0 || o.device >= ndev) return fail(NWK_EINVAL, "nwk_ctx_create: device %d of %d", o.device, ndev);
+  if (o.finalize < 0 || o.finalize > 2) return fail(NWK_EINVAL, "nwk_ctx_create: finalize must be 0/1/2");
   if (o.bits != 0 && o.bits != 4 && o.bits != 8 && o.bits != 16 && o.bits != 32)
     return fail(NWK_EINVAL, "nwk_ctx_create: bits must be 0/4/8/16/32");
   std::unique_ptr<nwk_ctx> c(new nwk_ctx);
@@ -246,6 +251,7 @@ int nwk_set_sequences(nwk_ctx* c, const uint8_t* seqs, const int64_t* offsets, i
   c->alpha = 0;
   for (int b = 0; b < 256; ++b)
     if (seen[b]) c->code_of[b] = (uint8_t)c->alpha++;
+  c->has_us = seen[(unsigned char)'_'];
   c->built[0] = c->built[1] = false;
   for (auto& b : c->built_sel) b = false;
   // layout: codes 8-aligned; E / SEL with kEPad entries before column 0 and kETail past the end
@@ -595,14 +601,23 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     void join() { if (t.joinable()) t.join(); }
     ~Joiner() { join(); }
   } fin;
+  // Device finalize (nw_hash) when no input byte is '_' and the
+  // batch has enough pairs for one lane per row to beat the host threads:
+  // est. device ms ~ 0.02 per 128-byte block of the longest row (per wave
+  // slot round), host ~ 350 bytes/us per thread.  NWK_DEVHASH=0/1 forces.
+  static const int devhash_env = getenv("NWK_DEVHASH") ? atoi(getenv("NWK_DEVHASH")) : -1;
+  const int fin_mode = c->opts.finalize == 1 ? 0 : c->opts.finalize == 2 ? 1 : devhash_env;
+  const bool dev_ok = a1 == nullptr && !c->has_us && fin_mode != 0;
+  if (dev_ok && !dp.empty() && (rc = build_encoding(c, 1)) != NWK_OK) return rc;
   size_t pos = 0;
+  double h_setup = 0, h_sync = 0, h_join = 0, h_last = 0;  // host phases (verbose)
   while (pos < dp.size()) {
     // ---- form a batch that fits the HBM budget
     size_t end = pos;
     int64_t mat = 0, bnd = 0, ops = 0, segops = 0;
     while (end < dp.size()) {
       const PairWork& w = dp[end];
-      const int64_t need = (mat + w.mat_dw) * 4 + (bnd + w.bnd_gr) * 8 + ops + w.ops_b + segops + w.segops_b + 4096;
+      const int64_t need = (mat + w.mat_dw) * 4 + (bnd + w.bnd_gr) * 8 + 3 * (ops + w.ops_b) + segops + w.segops_b + 8192;
       if (need > c->budget && end > pos) break;
       if (need > c->budget)
         return fail(NWK_ENOMEM, "pair %lld (%d x %d) needs %lld bytes > HBM budget %lld", (long long)w.id,
@@ -611,6 +626,20 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       ++end;
     }
     const int np = (int)(end - pos);
+    const double tb0 = now_ms();
+    bool devhash = false;
+    if (dev_ok) {
+      double bytes = 0, maxlen = 0;
+      for (size_t q = pos; q < end; ++q) {
+        bytes += 2.0 * (dp[q].m + dp[q].n);
+        maxlen = std::max(maxlen, (double)(dp[q].m + dp[q].n));
+      }
+      const double waves = 2.0 * np / 64.0, slots = 8.0 * c->cus;
+      const double est_dev = (maxlen / 128.0) * 0.02 * std::max(1.0, waves / slots);
+      const double est_host = bytes / (350e3 * c->host_threads);
+      devhash = fin_mode == 1 || est_dev < 0.5 * est_host;
+      st.device_finalized += devhash ? 1 : 0;
+    }
     // Layout: [granules | slack | matrices | op strings].  The granule region
     // always starts at offset 0, so across batches it only ever overlaps
     // older granules or zeros -- never stale matrix words, whose upper halves
@@ -620,7 +649,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     const int64_t mat_base_b = round_up(bnd_need_b, 256);
     const int64_t ops_base_b = round_up(mat_base_b + mat * 4, 256);
     const int64_t segops_base_b = round_up(ops_base_b + ops, 256);
-    const int64_t work_b = segops_base_b + segops + 256;  // + slack: traceback tile overrun of the last band
+    // device finalize rows (align1 | align2, op-region layout) + 256 B read slack each
+    const int64_t rows_base_b = round_up(segops_base_b + segops, 256);
+    const int64_t work_b = rows_base_b + 2 * (ops + 256) + 256;  // + slack: traceback tile overrun of the last band
     void* const old_work = c->d_work.p;
     if ((rc = c->d_work.ensure((size_t)work_b)) != NWK_OK) return rc;
     if (c->d_work.p != old_work) c->clean_b = 0;
@@ -754,7 +785,28 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     }
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(launch_fill(pl.mode, pl.bits, fa, std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     if (pl.mode == kPacked2) HIP_TRY(launch_gather(fa, np, c->stream));  // segment chains -> op strings
+    if (devhash) {
+      if ((rc = c->d_pen.ensure(4 * (size_t)np)) != NWK_OK) return rc;
+      if ((rc = c->d_hash.ensure(64 * (size_t)np)) != NWK_OK) return rc;
+      HashArgs ha;
+      ha.pairs = fa.pairs;
+      ha.npairs = np;
+      ha.raw = c->d_codes[1].as<uint8_t>();
+      ha.ops = fa.ops;
+      ha.ops_base = ops_base_b;
+      ha.rows1 = c->d_work.as<uint8_t>() + rows_base_b;
+      ha.rows2 = ha.rows1 + ops + 256;
+      ha.oplen = fa.oplen;
+      ha.endij = fa.endij;
+      ha.pxy = sc.pxy;
+      ha.gopen = sc.affine ? sc.go + sc.ge : sc.pgap;
+      ha.gext = sc.affine ? sc.ge : sc.pgap;
+      ha.penalties = c->d_pen.as<int>();
+      ha.hashes = c->d_hash.as<uint8_t>();
+      HIP_TRY(launch_hash(ha, c->stream));
+    }
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     if (c->opts.verbose >= 3) {
       fprintf(stderr, "nwk batch %d: launched mode %d bits %d grid %d, waiting\n", st.batches, pl.mode, pl.bits, grid);
@@ -781,9 +833,18 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipMemcpyAsync(&herr, fa.err, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_oplen[par].p, fa.oplen, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_endij[par].p, fa.endij, sizeof(int2) * np, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_ops[par].p, c->d_work.as<uint8_t>() + ops_base_b, (size_t)ops, hipMemcpyDeviceToHost,
-                           c->stream));
+    if (devhash) {  // 68 bytes per pair instead of the move strings
+      if ((rc = c->h_pen[par].ensure(4 * (size_t)np)) != NWK_OK) return rc;
+      if ((rc = c->h_hash[par].ensure(64 * (size_t)np)) != NWK_OK) return rc;
+      HIP_TRY(hipMemcpyAsync(c->h_pen[par].p, c->d_pen.p, 4 * (size_t)np, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipMemcpyAsync(c->h_hash[par].p, c->d_hash.p, 64 * (size_t)np, hipMemcpyDeviceToHost, c->stream));
+    } else {
+      HIP_TRY(hipMemcpyAsync(c->h_ops[par].p, c->d_work.as<uint8_t>() + ops_base_b, (size_t)ops,
+                             hipMemcpyDeviceToHost, c->stream));
+    }
+    const double tb1 = now_ms();
     HIP_TRY(hipStreamSynchronize(c->stream));
+    const double tb2 = now_ms();
     if (herr) {
       std::vector<unsigned> dn((size_t)np);
       (void)hipMemcpy(dn.data(), c->d_done.p, sizeof(unsigned) * np, hipMemcpyDeviceToHost);
@@ -797,8 +858,11 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       return fail(NWK_EKERNEL, "kernel hand-off timed out (err=%u); dequeued %u of %lld; done%s",
                   herr, cnt, (long long)ntasks, d.c_str());
     }
-    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[2]));
     st.fill_ms += ms;  // fill + fused traceback (one launch)
+    float ms2 = 0;
+    HIP_TRY(hipEventElapsedTime(&ms2, c->ev[2], c->ev[1]));
+    st.traceback_ms += ms2;  // after the fill: segment gather (kPacked2) + device finalize (nw_rows, nw_hash)
     if (fa.stamps) {  // per-pair timeline (100 MHz ticks), relative to the earliest fill-done
       std::vector<unsigned long long> sp(11 * (size_t)np + 1);
       HIP_TRY(hipMemcpy(sp.data(), fa.stamps, 88 * (size_t)np + 8, hipMemcpyDeviceToHost));
@@ -851,13 +915,22 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     // ---- host finalize, overlapped with the next batch's kernel: it runs on
     // its own thread over this batch's host buffer set while the loop goes
     // on to set up, launch and wait for batch b+1 (buffer set par ^ 1).
+    const double tj0 = now_ms();
     fin.join();
+    h_join += now_ms() - tj0;
     const int* ol = c->h_oplen[par].as<int>();
     const int2* ej = c->h_endij[par].as<int2>();
     const uint8_t* hops = c->h_ops[par].as<uint8_t>();
     const PairWork* dw = dp.data() + pos;
-    auto job = [c, a1, a2, np, dw, pd, ol, ej, hops, ops_base_b, sc, penalties, hashes, chain]() {
-      parallel_for(a1 ? 1 : c->host_threads, np, [&](int64_t q) {
+    const int* hpen = c->h_pen[par].as<int>();
+    const uint8_t* hhash = c->h_hash[par].as<uint8_t>();
+    auto job = [c, a1, a2, np, dw, pd, ol, ej, hops, ops_base_b, sc, penalties, hashes, chain, devhash, hpen, hhash]() {
+      if (devhash) {
+        for (int64_t q = 0; q < np; ++q) {
+          penalties[dw[q].out] = hpen[q];
+          memcpy(hashes + 64 * dw[q].out, hhash + 64 * q, 64);
+        }
+      } else parallel_for(a1 ? 1 : c->host_threads, np, [&](int64_t q) {
         const PairWork& w = dw[q];
         const PairDesc& d = pd[q];
         Finalized f;
@@ -872,11 +945,15 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       }
     };
     if (end < dp.size()) fin.start(job);
-    else job();
+    else { const double tf0 = now_ms(); job(); h_last += now_ms() - tf0; }
+    h_setup += tb1 - tb0;
+    h_sync += tb2 - tb1;
     pos = end;
   }
   fin.join();
   st.total_ms = now_ms() - t_start;
+  if (c->opts.verbose)
+    fprintf(stderr, "nwk host: setup+launch %.3f ms, kernel+copies wait %.3f ms, finalize join %.3f ms, last finalize %.3f ms\n", h_setup, h_sync, h_join, h_last);
   c->stats = st;
   if (c->opts.verbose)
     fprintf(stderr, "nwk: %zu pairs, %.3g cells, fill %.3f ms (%.1f GCUPS), traceback %.3f ms, total %.3f ms, bits %d mode %d, %d batch(es)\n",

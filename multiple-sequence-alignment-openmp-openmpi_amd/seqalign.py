@@ -35,7 +35,7 @@ class NwkError(RuntimeError):
 class Opts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("ngpus", ctypes.c_int32), ("bits", ctypes.c_int32),
                 ("host_threads", ctypes.c_int32), ("workspace_bytes", ctypes.c_int64),
-                ("verbose", ctypes.c_int32), ("reserved", ctypes.c_int32 * 5)]
+                ("verbose", ctypes.c_int32), ("finalize", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
 
 
 class Stats(ctypes.Structure):
@@ -43,7 +43,8 @@ class Stats(ctypes.Structure):
                 ("total_ms", ctypes.c_double), ("cells", ctypes.c_double),
                 ("matrix_bytes", ctypes.c_int64), ("batches", ctypes.c_int32),
                 ("bits", ctypes.c_int32), ("mode", ctypes.c_int32),
-                ("fill_launches", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
+                ("fill_launches", ctypes.c_int32), ("device_finalized", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 3)]
 
 
 # Every exported symbol of include/nwk.h with its ctypes signature.
@@ -137,12 +138,17 @@ def pair_ij(p):
 class Engine:
     """One device context: pooled HBM workspace + streams (nwk_ctx)."""
 
-    def __init__(self, device=0, bits=0, workspace_bytes=0, host_threads=0, verbose=False):
+    FINALIZE = {"auto": 0, "host": 1, "device": 2}
+
+    def __init__(self, device=0, bits=0, workspace_bytes=0, host_threads=0, verbose=False, finalize="auto"):
+        """finalize: where rows, penalty and SHA-512 of each pair are computed --
+        "auto" (per batch, by estimated cost), "host" threads, or "device" (nw_hash)."""
         self.lib = load_library()
         o = Opts()
         self.lib.nwk_opts_default(ctypes.byref(o))
         o.device, o.bits, o.workspace_bytes = device, bits, workspace_bytes
         o.host_threads, o.verbose = host_threads, int(verbose)
+        o.finalize = self.FINALIZE[finalize]
         self._ctx = ctypes.c_void_p()
         _check(self.lib.nwk_ctx_create(ctypes.byref(o), ctypes.byref(self._ctx)))
         self.k = 0

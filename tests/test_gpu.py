@@ -263,3 +263,61 @@ def test_align_all_multi_batch_affine():
     assert h == oh and [int(v) for v in pen] == opens
     ah, apens, _ = oracle.all_pairs_affine(genes, 3, 4, 1)
     assert ha == ah and [int(v) for v in pena] == apens
+
+
+# --- device finalize (nw_hash): rows, penalty and SHA-512 on the GPU
+
+@pytest.fixture(scope="module")
+def dev_engine():
+    e = seqalign.Engine(device=0, finalize="device")
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("case", [c for c in GOLDEN if c["name"] != "big13-2"], ids=lambda c: c["name"])
+def test_device_finalize_golden(dev_engine, case):
+    pxy, pgap, genes = case_input(case)
+    dev_engine.set_sequences(genes)
+    pen, hs = dev_engine.align_pairs(_all_ids(len(genes)), pxy, pgap)
+    assert [int(v) for v in pen] == case["penalties"]
+    if "pairs" in case:
+        assert [h.tobytes().hex() for h in hs] == [p["problemhash"] for p in case["pairs"]]
+    assert seqalign.chain_hash(hs) == case["hash"]
+    underscore = any(b"_" in g for g in genes)
+    used = dev_engine.stats()["device_finalized"]
+    if len(genes) > 1 and any(len(g) for g in genes):
+        assert used == (0 if underscore else 1), "device finalize must run (and only without '_' inputs)"
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_device_finalize_random_vs_oracle(dev_engine, seed):
+    r = random.Random(100 + seed)
+    # ragged lengths incl. 1-char and empty rows, long rows crossing many 128-byte SHA blocks
+    genes = _rand_genes(r, 9, 0, 3000, b"ACGT") + [b"A", b"", bytes(r.choice(b"ACGT") for _ in range(5000))]
+    for pxy, pgap in ((3, 2), (5, 1), (1, 4)):
+        dev_engine.set_sequences(genes)
+        pen, hs = dev_engine.align_pairs(_all_ids(len(genes)), pxy, pgap)
+        oh, opens, ohs = oracle.all_pairs(genes, pxy, pgap)
+        assert [int(v) for v in pen] == opens
+        assert [h.tobytes().hex() for h in hs] == ohs
+
+
+@pytest.mark.parametrize("go,ge", [(3, 1), (0, 2), (5, 2)])
+def test_device_finalize_affine_vs_oracle(dev_engine, go, ge):
+    r = random.Random(7 + go)
+    genes = _rand_genes(r, 7, 1, 2500, b"ACGT")
+    dev_engine.set_sequences(genes)
+    pen, hs = dev_engine.align_pairs_affine(_all_ids(len(genes)), 3, go, ge)
+    h, opens, ohs = oracle.all_pairs_affine(genes, 3, go, ge)
+    assert [int(v) for v in pen] == opens
+    assert [x.tobytes().hex() for x in hs] == ohs
+    assert dev_engine.stats()["device_finalized"] == 1
+
+
+def test_device_finalize_big13(dev_engine):
+    case = next(c for c in GOLDEN if c["name"] == "big13")
+    pxy, pgap, genes = case_input(case)
+    dev_engine.set_sequences(genes)
+    pen, hs = dev_engine.align_pairs(_all_ids(len(genes)), pxy, pgap)
+    assert [int(v) for v in pen] == case["penalties"]
+    assert seqalign.chain_hash(hs) == case["hash"]
