@@ -40,9 +40,11 @@ struct PairDesc {
   int32_t nchunks;  // ceil(n / 64): 64-column boundary chunks
   int32_t sblocks;  // 64-step super-blocks per band = nchunks + 1 (kPacked: + 2)
   int32_t slot;     // index of this pair in the batch's result arrays
-  // kPacked2 segmented traceback (see nw_align_pk2 / nw_gather)
+  // kPacked / kPacked2 segmented traceback (see run_segments / nw_gather)
   int32_t spec_every;   // a speculative segment after every spec_every-th task (0: whole-pair trace)
-  int64_t task_off;     // first entry of this pair in tdone / seginfo (one per task)
+  int32_t nguess;       // start columns per speculative boundary (segment id = task * nguess + guess)
+  int64_t task_off;     // first entry of this pair in tdone (one per task)
+  int64_t seg_off;      // first entry of this pair in seginfo (tasks * nguess)
   int64_t rec_off;      // first record of this pair in recs ([m / 128 + 1][2])
   int64_t segops_off;   // first byte of this pair's segment move buffers in segops
 };
@@ -73,9 +75,14 @@ struct FillArgs {
   int* seginfo;            // kPacked2: per task, 8 ints {len, ei, ej, mseg, midx, off lo, off hi, -}
   unsigned long long* recs;  // kPacked2: traceback record rows
   uint8_t* segops;         // kPacked2: segment move buffers
+  int2* tjobs;             // queued extra guesses {pair, segment id}
+  unsigned* tj_ready;      // per job: 1 = written
+  unsigned* tj_head;       // consumer counter
+  unsigned* tj_tail;       // producer counter
+  int ntjobs;              // jobs the batch will produce
 };
 
-constexpr int kMaxTasksPerPair = 2048;  // kPacked2 segment ids are 11 bits (m <= 2^21 rows)
+constexpr int kMaxSegsPerPair = 16384;  // segment ids are 14 bits in the traceback records
 
 // Device pair finalize (nwk_hash.hip): rows, penalty, problemhash per pair.
 struct HashArgs {
@@ -96,7 +103,7 @@ hipError_t launch_hash(const HashArgs& h, hipStream_t s);
 
 // Launchers (nwk_kernels.hip).  bits in {4, 8, 16, 32}.
 hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStream_t s);
-hipError_t launch_gather(const FillArgs& a, int npairs, hipStream_t s);
+hipError_t launch_gather(const FillArgs& a, int npairs, int task_shift, hipStream_t s);
 int fill_blocks_per_cu(int mode, int bits);
 
 // Dwords of one band of the stored matrix.

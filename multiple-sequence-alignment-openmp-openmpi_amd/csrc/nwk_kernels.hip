@@ -329,15 +329,17 @@ struct SegCtx {
   unsigned long long* recs;        // per pair [m / kRecRows + 1][2] records, nullptr: none
   const unsigned* tdone;           // per pair task-done flags, nullptr: all done
   int task_shift;                  // band -> task: b >> task_shift
+  const unsigned* resolved;        // speculative segments: the pair's chain is complete -> abort (mseg -4)
 };
 struct SegOut {
   int len, ei, ej;                 // moves, end cell
   int mseg, midx;                  // merged into segment mseg at its move midx (-1: ran to the border)
 };
 constexpr int kRecRows = 128;
-// record: bit 63 valid | column << 41 | segment << 30 | move index
+constexpr int kRecSlots = 32;  // per record row (open addressing by column; a full row just skips the check)
+// record: bit 63 valid | column (22 bits) << 41 | segment (14 bits) << 27 | move index (27 bits)
 __device__ __forceinline__ unsigned long long rec_pack(int col, int seg, int idx) {
-  return (1ull << 63) | ((unsigned long long)col << 41) | ((unsigned long long)seg << 30) | (unsigned long long)idx;
+  return (1ull << 63) | ((unsigned long long)col << 41) | ((unsigned long long)seg << 27) | (unsigned long long)idx;
 }
 
 template <int W, int LY = 0>
@@ -402,24 +404,31 @@ __device__ __forceinline__ SegOut trace_pair(const FillArgs& a, const PairDesc& 
     if (prof) tA = __builtin_amdgcn_s_memtime();
     if (sc.recs && (i & (kRecRows - 1)) == 0 && i != last_rec) {  // arrived on a record row
       last_rec = i;
-      unsigned long long* rp = sc.recs + 2 * (i / kRecRows);
+      // open-addressing table per record row keyed by column: any two
+      // segments that reach the same cell of this row find each other
+      unsigned long long* rp = sc.recs + (int64_t)kRecSlots * (i / kRecRows);
       int hit = -1;
       unsigned long long v0 = 0;
       if (lane == 0) {
         const unsigned long long mine = rec_pack(j, sc.seg, Lc);
-        for (int k = 0; k < 2 && hit < 0; ++k) {
-          unsigned long long v = __hip_atomic_load((gu64*)(rp + k), RLX_AGENT);
+        for (int k = 0; k < kRecSlots; ++k) {
+          unsigned long long* sp = rp + ((j + k) & (kRecSlots - 1));
+          unsigned long long v = __hip_atomic_load((gu64*)sp, RLX_AGENT);
           if (v == 0) {
-            v = atomicCAS((unsigned long long*)(rp + k), 0ull, mine);
-            if (v == 0) { hit = 2; break; }  // claimed: this segment owns the row's slot k
+            v = atomicCAS((unsigned long long*)sp, 0ull, mine);
+            if (v == 0) { hit = 2; break; }  // claimed: this segment owns the cell
           }
-          if ((int)((v >> 41) & 0x3fffff) == j) { hit = 1; v0 = v; }
+          if ((int)((v >> 41) & 0x3fffff) == j) { hit = 1; v0 = v; break; }
         }
       }
       hit = __builtin_amdgcn_readfirstlane(hit);
+      if (sc.resolved && __hip_atomic_load((gu32*)sc.resolved, RLX_AGENT) != 0u) {  // not on the final chain
+        mseg = -4;
+        break;
+      }
       if (hit == 1) {  // the owner passed through this very cell: same path from here on
-        mseg = __builtin_amdgcn_readfirstlane((int)((v0 >> 30) & 0x7ff));
-        midx = __builtin_amdgcn_readfirstlane((int)(v0 & 0x3fffffff));
+        mseg = __builtin_amdgcn_readfirstlane((int)((v0 >> 27) & 0x3fff));
+        midx = __builtin_amdgcn_readfirstlane((int)(v0 & 0x7ffffff));
         break;
       }
     }
@@ -431,6 +440,10 @@ __device__ __forceinline__ SegOut trace_pair(const FillArgs& a, const PairDesc& 
       const int s = Y::step(t, w & 7, j, Y::hb(b));
       if (b != tb || s < C::TS * tq || tl < tt0 || t >= tt0 + C::TL) {
         const int q = s / C::TS;
+        if (sc.resolved && __hip_atomic_load((gu32*)sc.resolved, RLX_AGENT) != 0u) {  // walks along a row
+          mseg = -4;                                                                   // cross no record row
+          break;
+        }
         if (sc.tdone && (b >> sc.task_shift) < task_ok) {  // entering rows of a task not yet seen done
           const int tsk = b >> sc.task_shift;
           const unsigned long long t0w = __builtin_amdgcn_s_memrealtime();
@@ -589,7 +602,7 @@ __device__ __forceinline__ SegOut trace_pair(const FillArgs& a, const PairDesc& 
 // Whole-pair trace from (m, n) into the pair's op buffer (nw_align, nw_align_pk).
 template <int W, int LY = 0>
 __device__ __forceinline__ void trace_whole(const FillArgs& a, const PairDesc& pd, TbLds<W, LY>& L, int lane) {
-  const SegOut o = trace_pair<W, LY>(a, pd, L, lane, SegCtx{a.ops + pd.ops_off, pd.m, pd.n, 0, nullptr, nullptr, 0});
+  const SegOut o = trace_pair<W, LY>(a, pd, L, lane, SegCtx{a.ops + pd.ops_off, pd.m, pd.n, 0, nullptr, nullptr, 0, nullptr});
   if (lane == 0) {
     a.oplen[pd.slot] = o.len;
     a.endij[pd.slot] = make_int2(o.ei, o.ej);
@@ -741,6 +754,134 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
 }
 
 
+// Segmented traceback (nw_align_pk / nw_align_pk2).  Segment ids are
+// task * NG + g: g = 0 is traced by the wave that filled the task (the
+// pair's last task: from (m, n); every spec_every-th task: speculatively from
+// the task's last row), g = 1 .. NG-1 are extra speculative start columns on
+// the same row, queued for waves that have no fill task left.  Paths from a
+// guessed cell coalesce with the true path only after ~5-15k rows; with
+// guesses spread between the diagonal and the proportional column one of
+// them is usually close and merges within ~1k rows.
+struct SegGeo {  // per kernel: rows per task and band -> task shift
+  int RT, task_shift;
+};
+__device__ __forceinline__ int guess_col(const PairDesc& pd, int R, int g) {
+  const int prop = max(1, (int)(((int64_t)pd.n * R) / pd.m));
+  if (g == 0 || pd.nguess < 3) return prop;
+  // candidates: start diagonal R, proportional, end-anchored diagonal R + n - m
+  // (DIAG > UP > LEFT from (m, n) tends to push the surplus gaps to the start)
+  const int endd = min(pd.n, max(1, R + pd.n - pd.m));
+  const int lo = min(min(R, prop), endd), hi = max(max(R, prop), endd);
+  const int mg = (hi - lo) / 4 + R / 16 + 64;
+  const int l2 = max(1, lo - mg), h2 = min(pd.n, hi + mg);
+  return l2 + (int)((int64_t)(h2 - l2) * (g - 1) / (pd.nguess - 2));
+}
+// move-buffer offset of segment (boundary k, guess g); the last task's segment is k = K, g = 0
+__device__ __forceinline__ int64_t seg_offset(const PairDesc& pd, int RT, int k, int g) {
+  const int64_t E = pd.spec_every, NG = pd.nguess;
+  return NG * (E * RT * k * (k + 1) / 2 + (int64_t)k * pd.n) + (int64_t)g * ((int64_t)(k + 1) * E * RT + pd.n);
+}
+template <int W, int LY>
+__device__ __forceinline__ void trace_segment(const FillArgs& a, const PairDesc& pd, TbLds<W, LY>& tb, int lane,
+                                              int task, int g, int ntp, SegGeo geo) {
+  const int E = pd.spec_every, NG = pd.nguess;
+  const bool last = task + 1 == ntp;
+  const int k = last ? (E > 0 ? (ntp - 1) / E : 0) : (task + 1) / E - 1;
+  const int64_t off = seg_offset(pd, geo.RT, k, g);
+  const int i0 = last ? pd.m : (task + 1) * geo.RT;
+  const int j0 = last ? pd.n : guess_col(pd, i0, g);
+  const int seg = task * NG + g;
+  // issue priority: fill 3 > the pair's own (last-task) trace 2 > speculation 0,
+  // so speculative walks only take cycles the critical-path waves leave idle
+  if (last) __builtin_amdgcn_s_setprio(2);
+  else __builtin_amdgcn_s_setprio(0);
+  if (last && a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
+  SegOut o{0, i0, j0, -1, 0};
+  if (a.dbg_notrace) {
+    o = SegOut{0, pd.m, pd.n, -1, 0};
+  } else {
+    const SegCtx sc{a.segops + pd.segops_off + off, i0, j0, seg, E > 0 ? a.recs + pd.rec_off : nullptr,
+                    a.tdone + pd.task_off, geo.task_shift, last ? nullptr : a.done + pd.slot};
+    o = trace_pair<W, LY>(a, pd, tb, lane, sc);
+  }
+  if (lane == 0) {
+    int* si = a.seginfo + 8 * (pd.seg_off + seg);
+    si[0] = o.len; si[1] = o.ei; si[2] = o.ej; si[3] = o.mseg; si[4] = o.midx;
+    si[5] = (int)(off & 0x7fffffff); si[6] = (int)(off >> 31);
+    // finished: publish, then see whether the chain from the pair's last-task
+    // segment is now complete (every hop finished, ending at the border)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store((gu32*)(si + 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (E > 0 && o.mseg != -4) {
+      int c = (ntp - 1) * NG;
+      for (int hop = 0; hop <= ntp * NG; ++hop) {
+        const int* sj = a.seginfo + 8 * (pd.seg_off + c);
+        if (__hip_atomic_load((gu32*)(sj + 7), RLX_AGENT) == 0u) break;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const int nx = __hip_atomic_load((gu32*)(sj + 3), RLX_AGENT);
+        if (nx == -1) {
+          __hip_atomic_store((gu32*)(a.done + pd.slot), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        if (nx < 0 || nx >= ntp * NG) break;
+        c = nx;
+      }
+    }
+  }
+  if (last && a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
+  if (a.stamps && lane == 0) {  // per pair: latest end of any segment, and its segment id
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long prev = atomicMax(a.stamps + 11 * a.ntasks_pairs + 1 + 2 * pd.slot, t);
+    if (t > prev) a.stamps[11 * a.ntasks_pairs + 2 + 2 * pd.slot] = ((unsigned long long)seg << 32) | (unsigned)o.len;
+  }
+}
+// Task `task` of pair q is filled and its stores released: flag it, queue
+// the extra guesses of its boundary, trace segment g = 0.
+template <int W, int LY>
+__device__ __forceinline__ void run_segments(const FillArgs& a, const PairDesc& pd, int q, TbLds<W, LY>& tb, int lane,
+                                             int task, int ntp, SegGeo geo) {
+  if (lane == 0) __hip_atomic_store((gu32*)(a.tdone + pd.task_off + task), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int E = pd.spec_every;
+  const bool last = task + 1 == ntp;
+  if (!(last || (E > 0 && (task + 1) % E == 0))) return;
+  if (!last && pd.nguess > 1) {
+    if (lane == 0) {
+      const unsigned s0 = atomicAdd(a.tj_tail, (unsigned)(pd.nguess - 1));
+      for (int g = 1; g < pd.nguess; ++g) a.tjobs[s0 + g - 1] = make_int2(q, task * pd.nguess + g);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      for (int g = 1; g < pd.nguess; ++g)
+        __hip_atomic_store((gu32*)(a.tj_ready + s0 + g - 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  trace_segment<W, LY>(a, pd, tb, lane, task, 0, ntp, geo);
+}
+// A wave with no fill task left traces queued extra guesses until all
+// a.ntjobs have been handed out (each is produced by a fill task that
+// finishes without waiting on any trace).
+template <int W, int LY>
+__device__ __forceinline__ void consume_guesses(const FillArgs& a, TbLds<W, LY>& tb, int lane, SegGeo geo) {
+  for (;;) {
+    unsigned h = 0;
+    if (lane == 0) h = atomicAdd(a.tj_head, 1u);
+    h = __builtin_amdgcn_readfirstlane(h);
+    if (h >= (unsigned)a.ntjobs) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load((gu32*)(a.tj_ready + h), RLX_AGENT) == 0u) {
+      __builtin_amdgcn_s_sleep(8);
+      if (__hip_atomic_load((gu32*)a.err, RLX_AGENT) != 0u) return;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
+        if (lane == 0) atomicOr(a.err, 128u);
+        return;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int2 job = a.tjobs[h];
+    const PairDesc pd = a.pairs[job.x];
+    const int ntp = (pd.nbands + (1 << geo.task_shift) - 1) >> geo.task_shift;
+    trace_segment<W, LY>(a, pd, tb, lane, job.y / pd.nguess, job.y % pd.nguess, ntp, geo);
+  }
+}
+
 // ===========================================================================
 // Packed fill (kPacked): the kProfile recurrence at W = 4 with two cells per
 // VGPR as int16 pairs.  On gfx950 v_pk_min_i16 / v_pk_add_u16 / v_perm_b32
@@ -858,13 +999,18 @@ __global__ __launch_bounds__(256) void nw_align_pk(FillArgs a) {
   const int wid = threadIdx.x >> 6;
   int* ring = ring_all[wid];
   unsigned* swin = swin_all[wid];
+  if (a.stamps && threadIdx.x == 0) atomicMin(a.stamps + 11 * a.ntasks_pairs, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 
   for (;;) {
     unsigned tk = 0;
     if (lane == 0) tk = atomicAdd(a.counter, 1u);
     tk = __builtin_amdgcn_readfirstlane(tk);
-    if (tk >= (unsigned)a.ntasks) return;
+    if (tk >= (unsigned)a.ntasks) {
+      if (a.ntjobs > 0) consume_guesses<W, 1>(a, tbl[wid], lane, SegGeo{kBandRows, 0});
+      return;
+    }
     if (__hip_atomic_load((gu32*)a.err, RLX_AGENT) != 0u) return;
+    __builtin_amdgcn_s_setprio(3);
     const int2 task = a.tasks[tk];
     const PairDesc pd = a.pairs[task.x];
     const int band = task.y;
@@ -969,20 +1115,7 @@ __global__ __launch_bounds__(256) void nw_align_pk(FillArgs a) {
       atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 1, (unsigned long long)n_wait);
       atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 2, (unsigned long long)pd.sblocks);
     }
-    unsigned prev = 0;
-    if (lane == 0) prev = __hip_atomic_fetch_add((gu32*)(a.done + pd.slot), 1u, RLX_AGENT);
-    prev = __builtin_amdgcn_readfirstlane(prev);
-    if (prev + 1u == (unsigned)pd.nbands) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
-      if (a.dbg_notrace) {  // debug (NWK_NOTRACE): fill-only timing, results invalid
-        if (lane == 0) { a.oplen[pd.slot] = 0; a.endij[pd.slot] = make_int2(pd.m, pd.n); }
-      } else {
-        trace_whole<W, 1>(a, pd, tbl[wid], lane);
-      }
-      if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
-    }
+    run_segments<W, 1>(a, pd, task.x, tbl[wid], lane, band, pd.nbands, SegGeo{kBandRows, 0});
   }
 }
 
@@ -1082,8 +1215,12 @@ __global__ __launch_bounds__(256) void nw_align_pk2(FillArgs a) {
     unsigned tk = 0;
     if (lane == 0) tk = atomicAdd(a.counter, 1u);
     tk = __builtin_amdgcn_readfirstlane(tk);
-    if (tk >= (unsigned)a.ntasks) return;
+    if (tk >= (unsigned)a.ntasks) {
+      if (a.ntjobs > 0) consume_guesses<W, 2>(a, tbl[wid], lane, SegGeo{2 * kBandRows, 1});
+      return;
+    }
     if (__hip_atomic_load((gu32*)a.err, RLX_AGENT) != 0u) return;
+    __builtin_amdgcn_s_setprio(3);
     const int2 task = a.tasks[tk];
     const PairDesc pd = a.pairs[task.x];
     const int bp = task.y;                    // band pair: bands 2bp, 2bp+1
@@ -1194,37 +1331,7 @@ __global__ __launch_bounds__(256) void nw_align_pk2(FillArgs a) {
       atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 1, (unsigned long long)n_wait);
       atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 2, (unsigned long long)pd.sblocks);
     }
-    // --- task done (its stores were released above); the pair's last task and
-    // every spec_every-th task then trace a segment (see SegCtx)
-    if (lane == 0) __hip_atomic_store((gu32*)(a.tdone + pd.task_off + bp), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int E = pd.spec_every;
-    const bool last = bp + 1 == ntp;
-    if (last || (E > 0 && (bp + 1) % E == 0)) {
-      constexpr int RT = 2 * kBandRows;  // rows per task
-      const int k = last ? (E > 0 ? (ntp - 1) / E : 0) : (bp + 1) / E - 1;
-      const int64_t off = (int64_t)E * RT * k * (k + 1) / 2 + (int64_t)k * pd.n;
-      int i0 = pd.m, j0 = pd.n;
-      if (!last) {  // guess: the proportional diagonal
-        i0 = (bp + 1) * RT;
-        j0 = (int)(((int64_t)pd.n * i0) / pd.m);
-        j0 = j0 < 1 ? 1 : j0;
-      }
-      if (last && a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
-      SegOut o{0, i0, j0, -1, 0};
-      if (a.dbg_notrace) {
-        o = SegOut{0, pd.m, pd.n, -1, 0};
-      } else {
-        const SegCtx sc{a.segops + pd.segops_off + off, i0, j0, bp, E > 0 ? a.recs + pd.rec_off : nullptr,
-                        a.tdone + pd.task_off, 1};
-        o = trace_pair<W, 2>(a, pd, tbl[wid], lane, sc);
-      }
-      if (lane == 0) {
-        int* si = a.seginfo + 8 * (pd.task_off + bp);
-        si[0] = o.len; si[1] = o.ei; si[2] = o.ej; si[3] = o.mseg; si[4] = o.midx;
-        si[5] = (int)(off & 0x7fffffff); si[6] = (int)(off >> 31);
-      }
-      if (last && a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
-    }
+    run_segments<W, 2>(a, pd, task.x, tbl[wid], lane, bp, ntp, SegGeo{2 * kBandRows, 1});
   }
 }
 
@@ -1232,43 +1339,42 @@ __global__ __launch_bounds__(256) void nw_align_pk2(FillArgs a) {
 // segment follow the merge links, copying [from, len) of every segment on the
 // way into the pair's contiguous op buffer; the end cell comes from the
 // segment that ran to the border.  One workgroup per pair.
-__global__ __launch_bounds__(256) void nw_gather(FillArgs a, int npairs) {
-  __shared__ int pc_seg[kMaxTasksPerPair], pc_from[kMaxTasksPerPair];
-  __shared__ int n_pc, fin_i, fin_j, bad;
+__global__ __launch_bounds__(256) void nw_gather(FillArgs a, int npairs, int task_shift) {
+  __shared__ int c_seg, c_from, c_len, c_done, c_bad, n_seg, n_from, fin_i, fin_j;
+  __shared__ long long c_off;
   const int q = blockIdx.x;
   if (q >= npairs) return;
   const PairDesc pd = a.pairs[q];
-  const int ntp = (pd.nbands + 1) >> 1;
-  if (threadIdx.x == 0) {
-    int s = ntp - 1, from = 0, n = 0;
-    bad = 0;
-    for (;;) {
-      const int* si = a.seginfo + 8 * (pd.task_off + s);
-      if (n >= ntp || si[3] == -2 || from < 0 || from > si[0]) { bad = 1; break; }
-      pc_seg[n] = s;
-      pc_from[n] = from;
-      ++n;
-      if (si[3] < 0) { fin_i = si[1]; fin_j = si[2]; break; }
-      from = si[4];
-      s = si[3];
-      if (s < 0 || s >= ntp) { bad = 1; break; }
-    }
-    n_pc = n;
-  }
-  __syncthreads();
-  if (bad) {
-    if (threadIdx.x == 0) atomicOr(a.err, 64u);
-    return;
-  }
+  const int ntp = (pd.nbands + (1 << task_shift) - 1) >> task_shift;
+  const int nseg = ntp * pd.nguess;
   uint8_t* out = a.ops + pd.ops_off;
+  if (threadIdx.x == 0) { n_seg = (ntp - 1) * pd.nguess; n_from = 0; }
   int pos = 0;
-  for (int c = 0; c < n_pc; ++c) {
-    const int* si = a.seginfo + 8 * (pd.task_off + pc_seg[c]);
-    const int64_t off = (int64_t)si[5] | ((int64_t)si[6] << 31);
-    const uint8_t* src = a.segops + pd.segops_off + off;
-    const int from = pc_from[c], len = si[0];
-    for (int t = from + threadIdx.x; t < len; t += blockDim.x) out[pos + t - from] = src[t];
-    pos += len - from;
+  for (int hop = 0;; ++hop) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      c_seg = n_seg;
+      c_from = n_from;
+      const int* si = a.seginfo + 8 * (pd.seg_off + c_seg);
+      c_len = si[0];
+      c_off = (long long)si[5] | ((long long)si[6] << 31);
+      c_done = si[3] < 0 ? 1 : 0;
+      c_bad = (hop > nseg || si[3] == -2 || c_from < 0 || c_from > c_len) ? 1 : 0;
+      fin_i = si[1];
+      fin_j = si[2];
+      n_seg = si[3];
+      n_from = si[4];
+      if (!c_done && (n_seg < 0 || n_seg >= nseg)) c_bad = 1;
+    }
+    __syncthreads();
+    if (c_bad) {
+      if (threadIdx.x == 0) atomicOr(a.err, 64u);
+      return;
+    }
+    const uint8_t* src = a.segops + pd.segops_off + c_off;
+    for (int t = c_from + threadIdx.x; t < c_len; t += blockDim.x) out[pos + t - c_from] = src[t];
+    pos += c_len - c_from;
+    if (c_done) break;
   }
   if (threadIdx.x == 0) {
     a.oplen[pd.slot] = pos;
@@ -1276,8 +1382,8 @@ __global__ __launch_bounds__(256) void nw_gather(FillArgs a, int npairs) {
   }
 }
 
-hipError_t launch_gather(const FillArgs& a, int npairs, hipStream_t s) {
-  hipLaunchKernelGGL(nw_gather, dim3(npairs), dim3(256), 0, s, a, npairs);
+hipError_t launch_gather(const FillArgs& a, int npairs, int task_shift, hipStream_t s) {
+  hipLaunchKernelGGL(nw_gather, dim3(npairs), dim3(256), 0, s, a, npairs, task_shift);
   return hipGetLastError();
 }
 

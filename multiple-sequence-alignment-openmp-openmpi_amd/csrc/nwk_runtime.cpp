@@ -118,7 +118,9 @@ struct PairWork {
   int m, n;
   int64_t mat_dw, bnd_gr, ops_b;  // footprint
   int64_t segops_b, segctl_b;     // kPacked2 segmented traceback: move buffers, control (flags, info, records)
-  int spec;                       // kPacked2: spec_every
+  int spec;                       // segmented traceback: spec_every
+  int nguess;                     // segmented traceback: start columns per speculative boundary
+  int64_t njobs;                  // queued extra guesses (spec boundaries x (nguess - 1))
 };
 
 }  // namespace
@@ -391,13 +393,20 @@ inline int64_t tasks_of(int mode, int64_t nb) { return mode == kPacked2 ? (nb + 
 // kPacked2 segmented traceback footprint for a speculative segment every E
 // tasks (E = 0: one whole-pair segment): move buffers (segment k starts on
 // row (k+1)*E*RT and may run to the border: capacity row + n) and control.
-void seg_footprint(PairWork* w, int E) {
-  const int64_t RT = 2 * kBandRows, nt = ceil_div(w->m, RT);
-  if (nt > kMaxTasksPerPair || w->n >= (1 << 22)) E = 0;  // record fields: 11-bit segment, 22-bit column
+inline bool segmented(int mode) { return mode == kPacked || mode == kPacked2; }
+
+void seg_footprint(PairWork* w, int mode, int E, int NG) {
+  const int64_t RT = mode == kPacked2 ? 2 * kBandRows : kBandRows, nt = ceil_div(w->m, RT);
+  if (w->n >= (1 << 22) || (int64_t)w->m + w->n >= (1 << 27)) E = 0;  // record fields: 22-bit column, 27-bit index
+  if (E <= 0) NG = 1;
+  while (NG > 1 && nt * NG > kMaxSegsPerPair) NG /= 2;     // 14-bit segment ids
+  if (nt > kMaxSegsPerPair) E = 0, NG = 1;
   const int64_t K = E > 0 ? (nt - 1) / E : 0;
   w->spec = E;
-  w->segops_b = round_up((int64_t)E * RT * K * (K + 1) / 2 + K * (int64_t)w->n + w->m + w->n, 16);
-  w->segctl_b = nt * (4 + 32) + (w->m / 128 + 1) * 16;
+  w->nguess = NG;
+  w->njobs = K * (NG - 1);
+  w->segops_b = round_up(NG * ((int64_t)E * RT * K * (K + 1) / 2 + K * (int64_t)w->n) + w->m + w->n, 16);
+  w->segctl_b = nt * 4 + nt * NG * 32 + (w->m / 128 + 1) * 32 * 8 + w->njobs * 12;  // records: 32 slots per 128th row
 }
 
 void footprint(PairWork* w, int bits, int mode, bool affine) {
@@ -406,7 +415,7 @@ void footprint(PairWork* w, int bits, int mode, bool affine) {
   const int64_t nt = tasks_of(mode, nb);
   w->segops_b = w->segctl_b = 0;
   w->spec = 0;
-  if (mode == kPacked2) seg_footprint(w, 0);
+  if (segmented(mode)) seg_footprint(w, mode, 0, 1);
   w->mat_dw = (mode == kPacked2 ? 2 * nt : nb) * band_dwords(bits, sblocks_of(mode, nch));
   w->bnd_gr = (nt - 1) * nch * 64 * (affine ? 2 : 1);  // affine: H and F boundary rows
   w->ops_b = round_up((int64_t)w->m + w->n, 16);
@@ -528,6 +537,16 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       if (((int64_t)w.m + w.n + 2) * ((int64_t)sc.go + sc.ge + sc.pxy) >= (1ll << 29))
         return fail(NWK_EINVAL, "affine scores of pair (%d x %d) would exceed the int32 range", w.m, w.n);
   }
+  // Small jobs (e.g. one rank's shard of a multi-GPU run): band-pair tasks
+  // (1024 rows, 16 cells per lane-step) too few to occupy the wave slots make
+  // each pair's row sweep the critical path -- single bands (nw_align_pk,
+  // 8 cells per lane-step) sweep a row in about half the time.
+  if (pl.mode == kPacked2 && !getenv("NWK_PACKED")) {
+    int64_t t2 = 0;
+    for (const auto& w : work)
+      if (w.m > 0 && w.n > 0) t2 += ceil_div(w.m, 2 * kBandRows);
+    if (t2 < 2 * 8 * (int64_t)c->cus) pl.mode = kPacked;
+  }
   st.bits = pl.bits;
   st.mode = pl.mode;
   int rc;
@@ -574,13 +593,21 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   // NWK_SPEC_FRAC (default 0.35) of the cells -- trace speculatively (a
   // segment every NWK_SPEC tasks, default 2); earlier pairs' whole-pair
   // traces overlap the remaining fill anyway.
-  if (pl.mode == kPacked2) {
+  if (segmented(pl.mode)) {
+    // small jobs (nw_align_pk chosen above): every pair's trace is on the
+    // critical path -> speculate everywhere with NWK_GUESS start columns per
+    // boundary (default 8); large jobs: only the tail pairs
+    const bool small = pl.mode == kPacked;
     static const int spec_env = getenv("NWK_SPEC") ? atoi(getenv("NWK_SPEC")) : 2;
-    static const double frac = getenv("NWK_SPEC_FRAC") ? atof(getenv("NWK_SPEC_FRAC")) : 0.35;
+    static const double frac_env = getenv("NWK_SPEC_FRAC") ? atof(getenv("NWK_SPEC_FRAC")) : -1.0;
+    static const int guess_env = getenv("NWK_GUESS") ? atoi(getenv("NWK_GUESS")) : 0;
+    const double frac = frac_env >= 0 ? frac_env : small ? 1.0 : 0.35;
+    const int NG = guess_env > 0 ? guess_env : small ? 8 : 1;
     double tot = 0, acc = 0;
     for (const auto& w : dp) tot += (double)w.m * w.n;
     for (auto& w : dp) {
-      seg_footprint(&w, acc >= (1.0 - frac) * tot ? std::max(0, spec_env) : 0);
+      const bool on = acc >= (1.0 - frac) * tot - 0.5;
+      seg_footprint(&w, pl.mode, on ? std::max(0, spec_env) * (pl.mode == kPacked ? 2 : 1) : 0, NG);
       acc += (double)w.m * w.n;
     }
   }
@@ -663,7 +690,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     const int par = st.batches & 1;  // host buffer set of this batch
     if ((rc = c->h_pairs[par].ensure(sizeof(PairDesc) * np)) != NWK_OK) return rc;
     PairDesc* pd = c->h_pairs[par].as<PairDesc>();
-    int64_t mo = 0, bo = 0, oo = 0, ntasks = 0, so = 0, ro = 0;
+    int64_t mo = 0, bo = 0, oo = 0, ntasks = 0, so = 0, ro = 0, nsegs = 0, njobs = 0;
     int maxb = 0;
     for (int q = 0; q < np; ++q) {
       const PairWork& w = dp[pos + q];
@@ -681,10 +708,14 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       d.sblocks = sblocks_of(pl.mode, d.nchunks);
       d.slot = q;
       d.spec_every = w.spec;
-      d.task_off = ntasks;  // one tdone / seginfo entry per task
+      d.nguess = w.nguess;
+      d.task_off = ntasks;  // one tdone entry per task
+      d.seg_off = nsegs;    // nguess seginfo entries per task
+      nsegs += tasks_of(pl.mode, d.nbands) * w.nguess;
+      njobs += w.njobs;
       d.rec_off = ro;
       d.segops_off = so;
-      ro += 2 * (w.m / 128 + 1);
+      ro += 32 * (w.m / 128 + 1);
       so += w.segops_b;
       mo += w.mat_dw; bo += w.bnd_gr; oo += w.ops_b;
       ntasks += tasks_of(pl.mode, d.nbands);
@@ -726,9 +757,14 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipMemcpyAsync(c->d_tasks.p, tk, sizeof(int2) * ntasks, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(c->d_ctl.p, 0, 256, c->stream));
     HIP_TRY(hipMemsetAsync(c->d_done.p, 0, sizeof(unsigned) * np, c->stream));
-    const int64_t rec_base_b = round_up(ntasks * (4 + 32), 8);  // [tdone u32 | seginfo 8 x int | recs u64]
-    const int64_t segctl_b = rec_base_b + ro * 8;
-    if (pl.mode == kPacked2) {
+    // [tdone u32 | seginfo 8 x int | recs u64 | job ready u32 | head, tail | jobs int2]
+    const int64_t seginfo_base_b = ntasks * 4;
+    const int64_t rec_base_b = round_up(seginfo_base_b + nsegs * 32, 8);
+    const int64_t tjr_base_b = rec_base_b + ro * 8;
+    const int64_t tjc_base_b = tjr_base_b + njobs * 4;
+    const int64_t tj_base_b = round_up(tjc_base_b + 8, 8);
+    const int64_t segctl_b = tj_base_b + njobs * 8;
+    if (segmented(pl.mode)) {
       if ((rc = c->d_segctl.ensure((size_t)segctl_b)) != NWK_OK) return rc;
       HIP_TRY(hipMemsetAsync(c->d_segctl.p, 0, (size_t)segctl_b, c->stream));
     }
@@ -763,15 +799,22 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.stamps = nullptr;
     fa.ntasks_pairs = np;
     if (c->opts.verbose >= 2) {
-      if ((rc = c->d_stamps.ensure(88 * (size_t)np + 16)) != NWK_OK) return rc;
+      if ((rc = c->d_stamps.ensure(88 * (size_t)np + 16 + 16 * (size_t)np)) != NWK_OK) return rc;
+      HIP_TRY(hipMemsetAsync(c->d_stamps.as<uint8_t>() + 88 * (size_t)np + 8, 0, 16 * (size_t)np, c->stream));
       HIP_TRY(hipMemsetAsync(c->d_stamps.p, 0, 88 * (size_t)np, c->stream));
       HIP_TRY(hipMemsetAsync(c->d_stamps.as<uint8_t>() + 88 * (size_t)np, 0xff, 8, c->stream));  // kernel start: atomicMin
       fa.stamps = c->d_stamps.as<unsigned long long>();
     }
     fa.ops = c->d_work.as<uint8_t>();
-    fa.tdone = pl.mode == kPacked2 ? c->d_segctl.as<unsigned>() : nullptr;
-    fa.seginfo = pl.mode == kPacked2 ? reinterpret_cast<int*>(c->d_segctl.as<uint8_t>() + ntasks * 4) : nullptr;
-    fa.recs = pl.mode == kPacked2 ? reinterpret_cast<unsigned long long*>(c->d_segctl.as<uint8_t>() + rec_base_b) : nullptr;
+    const bool seg = segmented(pl.mode);
+    fa.tdone = seg ? c->d_segctl.as<unsigned>() : nullptr;
+    fa.seginfo = seg ? reinterpret_cast<int*>(c->d_segctl.as<uint8_t>() + seginfo_base_b) : nullptr;
+    fa.recs = seg ? reinterpret_cast<unsigned long long*>(c->d_segctl.as<uint8_t>() + rec_base_b) : nullptr;
+    fa.tj_ready = seg ? reinterpret_cast<unsigned*>(c->d_segctl.as<uint8_t>() + tjr_base_b) : nullptr;
+    fa.tj_head = seg ? reinterpret_cast<unsigned*>(c->d_segctl.as<uint8_t>() + tjc_base_b) : nullptr;
+    fa.tj_tail = seg ? fa.tj_head + 1 : nullptr;
+    fa.tjobs = seg ? reinterpret_cast<int2*>(c->d_segctl.as<uint8_t>() + tj_base_b) : nullptr;
+    fa.ntjobs = seg ? (int)njobs : 0;
     fa.segops = c->d_work.as<uint8_t>() + segops_base_b;
     fa.oplen = c->d_oplen.as<int>();
     fa.endij = c->d_endij.as<int2>();
@@ -786,7 +829,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(launch_fill(pl.mode, pl.bits, fa, std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-    if (pl.mode == kPacked2) HIP_TRY(launch_gather(fa, np, c->stream));  // segment chains -> op strings
+    if (seg) HIP_TRY(launch_gather(fa, np, pl.mode == kPacked2 ? 1 : 0, c->stream));  // segment chains -> op strings
     if (devhash) {
       if ((rc = c->d_pen.ensure(4 * (size_t)np)) != NWK_OK) return rc;
       if ((rc = c->d_hash.ensure(64 * (size_t)np)) != NWK_OK) return rc;
@@ -864,13 +907,22 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipEventElapsedTime(&ms2, c->ev[2], c->ev[1]));
     st.traceback_ms += ms2;  // after the fill: segment gather (kPacked2) + device finalize (nw_rows, nw_hash)
     if (fa.stamps) {  // per-pair timeline (100 MHz ticks), relative to the earliest fill-done
-      std::vector<unsigned long long> sp(11 * (size_t)np + 1);
-      HIP_TRY(hipMemcpy(sp.data(), fa.stamps, 88 * (size_t)np + 8, hipMemcpyDeviceToHost));
+      std::vector<unsigned long long> sp(13 * (size_t)np + 1);
+      HIP_TRY(hipMemcpy(sp.data(), fa.stamps, 104 * (size_t)np + 8, hipMemcpyDeviceToHost));
       unsigned long long t0 = ~0ull, tlast = 0;
       for (int q = 0; q < np; ++q) t0 = std::min(t0, sp[8 * q]), tlast = std::max(tlast, sp[8 * q]);
       const unsigned long long tk0 = sp[11 * (size_t)np];
       fprintf(stderr, "nwk timeline: first pair filled %.3f ms, last pair filled %.3f ms after the kernel's first dequeue\n",
               (t0 - tk0) / 1e5, (tlast - tk0) / 1e5);
+      if (segmented(pl.mode)) {
+        fprintf(stderr, "nwk timeline: latest segment end per pair (ms after first dequeue; segment task.guess, moves):");
+        for (int q = 0; q < np; ++q) {
+          const unsigned long long te = sp[11 * (size_t)np + 1 + 2 * q], id = sp[11 * (size_t)np + 2 + 2 * q];
+          const int sg = (int)(id >> 32), ng = std::max(1, pd[q].nguess);
+          if (te) fprintf(stderr, " %d:%.2f(t%d.%d,%u)", q, (te - tk0) / 1e5, sg / ng, sg % ng, (unsigned)id);
+        }
+        fprintf(stderr, "\n");
+      }
       fprintf(stderr, "nwk timeline (ms after first pair filled; kernel %.3f ms): pair m x n: filled -> traced | "
                       "trace cycles switch/blocks, blocks, switches/walk-cycles | fill band-cycles, %% waiting on band above\n", ms);
       double bc = 0, wc = 0;
@@ -882,8 +934,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
                 pd[q].m, pd[q].n, (x[0] - t0) / 1e5, (x[1] - t0) / 1e5, (x[1] - x[0]) / 1e5, (double)x[2], (double)x[3],
                 x[4], x[5] >> 32, x[5] & 0xffffffffull, (double)x[6], x[6] ? 100.0 * (double)x[7] / (double)x[6] : 0.0);
       }
-      if (pl.mode == kPacked2 && getenv("NWK_SEGDUMP")) {  // segment outcomes of the pairs traced last
-        std::vector<int> si((size_t)ntasks * 8);
+      if (segmented(pl.mode) && getenv("NWK_SEGDUMP")) {  // segment outcomes of the pairs traced last
+        std::vector<int> si((size_t)nsegs * 8);
         HIP_TRY(hipMemcpy(si.data(), fa.seginfo, si.size() * 4, hipMemcpyDeviceToHost));
         std::vector<int> ord(np);
         for (int q = 0; q < np; ++q) ord[q] = q;
@@ -892,9 +944,23 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
           const int q = ord[z];
           const int nt = (int)tasks_of(pl.mode, pd[q].nbands);
           fprintf(stderr, "segments of pair %d (%d x %d, spec every %d):", q, pd[q].m, pd[q].n, pd[q].spec_every);
-          for (int b = 0; b < nt; ++b) {
-            const int* x = &si[8 * ((size_t)pd[q].task_off + b)];
-            if (x[0] || b == nt - 1) fprintf(stderr, " [t%d len %d end (%d,%d) -> %d@%d]", b, x[0], x[1], x[2], x[3], x[4]);
+          for (int b = 0; b < nt * pd[q].nguess; ++b) {
+            const int* x = &si[8 * ((size_t)pd[q].seg_off + b)];
+            if (x[0] || b == (nt - 1) * pd[q].nguess)
+              fprintf(stderr, " [t%d.%d len %d end (%d,%d) -> %d@%d]", b / pd[q].nguess, b % pd[q].nguess, x[0], x[1], x[2], x[3], x[4]);
+          }
+          fprintf(stderr, "\n");
+        }
+        for (int q = 0; q < np; ++q) {  // the resolved chain of every pair
+          const int nt = (int)tasks_of(pl.mode, pd[q].nbands), ng = pd[q].nguess;
+          int sgi = (nt - 1) * ng, from = 0;
+          fprintf(stderr, "chain of pair %d:", q);
+          for (int hop = 0; hop < 64; ++hop) {
+            const int* x = &si[8 * ((size_t)pd[q].seg_off + sgi)];
+            fprintf(stderr, " t%d.%d[%d..%d)", sgi / ng, sgi % ng, from, x[0]);
+            if (x[3] < 0) break;
+            from = x[4];
+            sgi = x[3];
           }
           fprintf(stderr, "\n");
         }

@@ -4,6 +4,14 @@
 //   stdin : pxy pgap k seq_0 ... seq_{k-1}   (whitespace-separated tokens)
 //   stdout: "Time: <us> us" / answer hash / penalties each followed by ' '
 //
+// Extensions (stdout unchanged):
+//   --fasta FILE --pxy P --pgap G   sequences from a FASTA file instead of stdin
+//                                   (records in file order; header lines start
+//                                   with '>', sequence lines concatenated with
+//                                   whitespace removed)
+//   --dump FILE                     per pair in canonical order: "i j penalty",
+//                                   then align1 and align2 (trimmed rows) lines
+//
 // The timed span is the getMinimumPenalties call (skel:53-61), here
 // nwk_get_minimum_penalties.  No MPI: the reference's ranks become devices
 // (--gpus N or NWK_GPUS=N); flags and statistics never change stdout.
@@ -12,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <iostream>
 #include <string>
 #include <vector>
@@ -24,27 +33,91 @@ static uint64_t GetTimeStamp() {
   return tv.tv_sec * (uint64_t)1000000 + tv.tv_usec;
 }
 
+// FASTA records in file order (see header).
+static bool read_fasta(const char* path, std::vector<std::string>* out) {
+  std::ifstream in(path, std::ios::binary);
+  if (!in) return false;
+  std::string line;
+  bool any = false;
+  while (std::getline(in, line)) {
+    if (!line.empty() && line[0] == '>') {
+      out->emplace_back();
+      any = true;
+      continue;
+    }
+    if (line.empty() || line[0] == ';') continue;
+    if (!any) {  // sequence text before the first header: an unnamed record
+      out->emplace_back();
+      any = true;
+    }
+    for (char ch : line)
+      if (!isspace((unsigned char)ch)) out->back().push_back(ch);
+  }
+  return true;
+}
+
+// Rows of every pair (one device, single-pair entry point) into `path`.
+static int dump_pairs(const char* path, const std::vector<std::string>& genes, int pxy, int pgap) {
+  FILE* f = fopen(path, "w");
+  if (!f) return NWK_EINVAL;
+  nwk_ctx* ctx = nullptr;
+  int rc = nwk_ctx_create(nullptr, &ctx);
+  for (size_t i = 1; rc == NWK_OK && i < genes.size(); ++i)
+    for (size_t j = 0; rc == NWK_OK && j < i; ++j) {
+      const std::string &x = genes[i], &y = genes[j];
+      std::vector<uint8_t> a1(x.size() + y.size() + 1), a2(x.size() + y.size() + 1);
+      int32_t alen = 0, pen = 0;
+      rc = nwk_get_minimum_penalty(ctx, reinterpret_cast<const uint8_t*>(x.data()), (int32_t)x.size(),
+                                   reinterpret_cast<const uint8_t*>(y.data()), (int32_t)y.size(), pxy, pgap,
+                                   a1.data(), a2.data(), &alen, &pen);
+      if (rc == NWK_OK)
+        fprintf(f, "%zu %zu %d\n%.*s\n%.*s\n", i, j, pen, alen, (const char*)a1.data(), alen, (const char*)a2.data());
+    }
+  nwk_ctx_destroy(ctx);
+  fclose(f);
+  return rc;
+}
+
 int main(int argc, char** argv) {
   nwk_opts o;
   nwk_opts_default(&o);
   if (const char* g = getenv("NWK_GPUS")) o.ngpus = atoi(g);
   if (const char* v = getenv("NWK_VERBOSE")) o.verbose = atoi(v);
   if (const char* b = getenv("NWK_BITS")) o.bits = atoi(b);
+  const char *fasta = nullptr, *dump = nullptr;
+  int fpxy = 3, fpgap = 2;
   for (int a = 1; a < argc; ++a) {
     if (!strcmp(argv[a], "--gpus") && a + 1 < argc) o.ngpus = atoi(argv[++a]);
     else if (!strcmp(argv[a], "--verbose")) o.verbose = 1;
     else if (!strcmp(argv[a], "--bits") && a + 1 < argc) o.bits = atoi(argv[++a]);
+    else if (!strcmp(argv[a], "--fasta") && a + 1 < argc) fasta = argv[++a];
+    else if (!strcmp(argv[a], "--pxy") && a + 1 < argc) fpxy = atoi(argv[++a]);
+    else if (!strcmp(argv[a], "--pgap") && a + 1 < argc) fpgap = atoi(argv[++a]);
+    else if (!strcmp(argv[a], "--dump") && a + 1 < argc) dump = argv[++a];
     else {
-      fprintf(stderr, "usage: %s [--gpus N] [--bits W] [--verbose] < input\n", argv[0]);
+      fprintf(stderr,
+              "usage: %s [--gpus N] [--bits W] [--verbose] [--fasta FILE --pxy P --pgap G] [--dump FILE] [< input]\n",
+              argv[0]);
       return 2;
     }
   }
   std::ios::sync_with_stdio(false);
   int misMatchPenalty = 0, gapPenalty = 0, k = 0;
-  std::cin >> misMatchPenalty >> gapPenalty >> k;
-  if (k < 0) k = 0;
-  std::vector<std::string> genes((size_t)k);
-  for (int i = 0; i < k; i++) std::cin >> genes[i];
+  std::vector<std::string> genes;
+  if (fasta) {
+    if (!read_fasta(fasta, &genes)) {
+      fprintf(stderr, "seqalkway: cannot read %s\n", fasta);
+      return 1;
+    }
+    misMatchPenalty = fpxy;
+    gapPenalty = fpgap;
+    k = (int)genes.size();
+  } else {
+    std::cin >> misMatchPenalty >> gapPenalty >> k;
+    if (k < 0) k = 0;
+    genes.resize((size_t)k);
+    for (int i = 0; i < k; i++) std::cin >> genes[i];
+  }
   std::vector<int64_t> off((size_t)k + 1, 0);
   for (int i = 0; i < k; i++) off[i + 1] = off[i] + (int64_t)genes[i].size();
   std::string all;
@@ -67,5 +140,9 @@ int main(int argc, char** argv) {
   std::cout << hash << std::endl;
   for (int64_t i = 0; i < numPairs; i++) std::cout << penalties[i] << " ";
   std::cout << std::endl;
+  if (dump && (rc = dump_pairs(dump, genes, misMatchPenalty, gapPenalty)) != NWK_OK) {
+    fprintf(stderr, "seqalkway: --dump: error %d: %s\n", rc, nwk_last_error());
+    return 1;
+  }
   return 0;
 }

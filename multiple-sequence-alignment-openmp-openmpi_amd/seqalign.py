@@ -310,6 +310,37 @@ def getMinimumPenalty(x, y, pxy, pgap, device=0):
         return e.get_minimum_penalty(x, y, pxy, pgap)
 
 
+def parse_fasta(text):
+    """FASTA records in file order: header lines start with '>',
+    sequence lines are concatenated with whitespace removed, ';' lines are
+    comments; sequence text before the first header is an unnamed record.
+    Same rules as the driver's --fasta (csrc/seqalkway_main.cpp read_fasta)."""
+    if isinstance(text, str):
+        text = text.encode("latin-1")
+    genes, cur = [], None
+    for line in text.split(b"\n"):
+        if line.startswith(b">"):
+            cur = bytearray()
+            genes.append(cur)
+            continue
+        if not line.strip() or line.startswith(b";"):
+            continue
+        if cur is None:
+            cur = bytearray()
+            genes.append(cur)
+        cur += b"".join(line.split())
+    return [bytes(g) for g in genes]
+
+
+def read_input(path, pxy=3, pgap=2):
+    """(pxy, pgap, genes) from the reference's token format, or from FASTA
+    (first non-blank character '>') with the given penalties."""
+    data = open(path, "rb").read()
+    if data.lstrip().startswith(b">"):
+        return pxy, pgap, parse_fasta(data)
+    return parse_input(data)
+
+
 def parse_input(text):
     """Rank-0 stdin parse of skel:40-47 (cin >> tokens): (pxy, pgap, genes)."""
     if isinstance(text, str):

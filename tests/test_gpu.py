@@ -284,9 +284,10 @@ def test_device_finalize_golden(dev_engine, case):
         assert [h.tobytes().hex() for h in hs] == [p["problemhash"] for p in case["pairs"]]
     assert seqalign.chain_hash(hs) == case["hash"]
     underscore = any(b"_" in g for g in genes)
-    used = dev_engine.stats()["device_finalized"]
+    st = dev_engine.stats()
     if len(genes) > 1 and any(len(g) for g in genes):
-        assert used == (0 if underscore else 1), "device finalize must run (and only without '_' inputs)"
+        assert st["device_finalized"] == (0 if underscore else st["batches"]), \
+            "device finalize must run on every batch (and only without '_' inputs)"
 
 
 @pytest.mark.parametrize("seed", range(4))
@@ -321,3 +322,27 @@ def test_device_finalize_big13(dev_engine):
     pen, hs = dev_engine.align_pairs(_all_ids(len(genes)), pxy, pgap)
     assert [int(v) for v in pen] == case["penalties"]
     assert seqalign.chain_hash(hs) == case["hash"]
+
+
+def test_driver_fasta_and_dump(golden, tmp_path):
+    """--fasta gives the same stdout as the token input; --dump rows match the oracle."""
+    c = golden["mseq1"]
+    text = open(os.path.join(GOLDEN_DIR, "data", c["file"]), "rb").read()
+    pxy, pgap, genes = seqalign.parse_input(text)
+    fa = tmp_path / "mseq1.fa"
+    # wrapped at 7 columns, with headers and a blank line
+    fa.write_bytes(b"".join(b">seq%d\n" % i + b"\n".join(g[k:k + 7] for k in range(0, len(g), 7)) + b"\n\n"
+                            for i, g in enumerate(genes)))
+    dump = tmp_path / "pairs.txt"
+    out = subprocess.run([os.path.join(PKG, "bin", "seqalkway"), "--fasta", str(fa), "--pxy", str(pxy),
+                          "--pgap", str(pgap), "--dump", str(dump)], stdout=subprocess.PIPE, check=True,
+                         timeout=300).stdout.decode().split("\n")
+    assert out[1] == c["hash"] and out[2] == "".join("%d " % p for p in c["penalties"])
+    lines = dump.read_bytes().split(b"\n")
+    p = 0
+    for i in range(1, len(genes)):
+        for j in range(i):
+            pen, a1, a2 = oracle.pair(genes[i], genes[j], pxy, pgap)
+            assert lines[3 * p] == b"%d %d %d" % (i, j, pen)
+            assert lines[3 * p + 1] == a1 and lines[3 * p + 2] == a2
+            p += 1

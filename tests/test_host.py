@@ -124,3 +124,20 @@ def test_no_device_fails_loudly(lib):
     assert e.value.code == -3
     with pytest.raises(seqalign.NwkError):
         seqalign.getMinimumPenalties([b"AC", b"CA"], 2, 3, 2, [0])
+
+
+def test_parse_fasta_records():
+    """FASTA input -- records in order, wrapped lines joined, blanks/comments skipped."""
+    text = b">s1 first\nACGT\nAC GT\n\n>s2\n;comment\nTTTT\n>empty\n>s4\r\nGG\r\n"
+    assert seqalign.parse_fasta(text) == [b"ACGTACGT", b"TTTT", b"", b"GG"]
+    assert seqalign.parse_fasta(b"ACG\nT\n>x\nA\n") == [b"ACGT", b"A"]
+    assert seqalign.parse_fasta(b"") == []
+
+
+def test_read_input_detects_fasta(tmp_path):
+    p = tmp_path / "in.fa"
+    p.write_bytes(b"\n>a\nACGT\n>b\nAGT\n")
+    assert seqalign.read_input(str(p), 5, 1) == (5, 1, [b"ACGT", b"AGT"])
+    q = tmp_path / "in.txt"
+    q.write_bytes(b"3 2 2\nACGT\nAGT\n")
+    assert seqalign.read_input(str(q)) == (3, 2, [b"ACGT", b"AGT"])
