@@ -545,7 +545,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     int64_t t2 = 0;
     for (const auto& w : work)
       if (w.m > 0 && w.n > 0) t2 += ceil_div(w.m, 2 * kBandRows);
-    if (t2 < 2 * 8 * (int64_t)c->cus) pl.mode = kPacked;
+    if (t2 < 8 * (int64_t)c->cus) pl.mode = kPacked;  // (2048 on 256 CUs; the kernels tie near there)
   }
   st.bits = pl.bits;
   st.mode = pl.mode;

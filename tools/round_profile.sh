@@ -21,5 +21,5 @@ run pmc_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/pmc_fetch -o
 run pmc_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/pmc_write -o p --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
 run bench_c4 300 python3 bench.py --workload c4 --steps 3 --warmup 1
 run bench_c3 400 python3 bench.py --workload c3 --steps 2 --warmup 1
-run bench_c5 500 python3 bench.py --workload c5 --steps 1 --warmup 1
+#run bench_c5 500 python3 bench.py --workload c5 --steps 1 --warmup 1
 echo done
