@@ -160,6 +160,23 @@ int nwk_get_minimum_penalties_affine(const uint8_t *seqs, const int64_t *offsets
                                      char *hash_hex, const nwk_opts *opts);
 
 /*
+ * Progressive sum-of-pairs MSA of the context's sequences (SURVEY.md §8 f3 --
+ * the reference stops at the pairwise penalties, skel:117-175, so the build
+ * defines it; oracle/msa_oracle.c nwo_msa is the restatement it must equal):
+ * UPGMA guide tree on `penalties` (the P pairwise penalties in canonical order,
+ * e.g. from nwk_align_all with the same pxy, pgap), then one profile-profile
+ * Needleman-Wunsch per merge under SoP costs (c(a,a) = 0, c(a,b) = pxy,
+ * c(a,'_') = pgap, c('_','_') = 0), traceback DIAG > UP > LEFT; merges of
+ * independent subtrees run in one launch.  Writes the k aligned rows (row r
+ * at rows + r*cap, '_' = gap), the MSA length and its SoP score.  For k = 2
+ * the rows are the reference's alignment of pair (1, 0).
+ * Requires pxy, pgap >= 0, no '_' in the input and at most 5 distinct bytes
+ * (NWK_EINVAL otherwise); cap >= the MSA length (<= the summed lengths).
+ */
+int nwk_msa(nwk_ctx *ctx, int32_t pxy, int32_t pgap, const int32_t *penalties, uint8_t *rows,
+            int64_t cap, int64_t *len, int64_t *sop);
+
+/*
  * Deterministic cell-cost shard of the P pairs of a sequence set over world
  * ranks (LPT on m*n, ties by pair id).  Writes this rank's pair ids
  * (ascending) to out_ids (capacity P) and their count to *out_n.

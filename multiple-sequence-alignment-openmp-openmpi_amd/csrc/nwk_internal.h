@@ -24,6 +24,7 @@ enum Mode : int {
   kAffine = 3,   // affine gaps: 4-bit traceback codes, compare mode
   kPacked = 4,   // kProfile at W = 4 with two cells per register (int16 pairs), packed layout
   kPacked2 = 5,  // kPacked with two bands per wave (band pairs), layout LY 2
+  kProfileDP = 6,  // profile-profile sum-of-pairs DP of the progressive MSA, 4-bit codes
 };
 
 // One pair of the batch.  All offsets are element offsets into the
@@ -80,7 +81,10 @@ struct FillArgs {
   unsigned* tj_head;       // consumer counter
   unsigned* tj_tail;       // producer counter
   int ntjobs;              // jobs the batch will produce
+  const int* prow;         // kProfileDP: per X column (DP row) 8 ints {rc[0..5], gx, H[i][0]} at pairs[].x_off
+  const int* pcol;         // kProfileDP: per Y column (DP column) 8 ints {cnt[0..5], gy, H[0][j]} at pairs[].y_off
 };
+constexpr int kProfSyms = 6;  // kProfileDP: symbols + gap per column profile
 
 constexpr int kMaxSegsPerPair = 16384;  // segment ids are 14 bits in the traceback records
 

@@ -1726,6 +1726,153 @@ __global__ __launch_bounds__(256) void nw_align_affine(FillArgs a) {
   }
 }
 
+// ===========================================================================
+// Profile-profile fill of the progressive SoP MSA (oracle
+// msa_oracle.c nwo_profile_align):
+//   H = min(H[i-1][j-1] + sub(i,j), H[i-1][j] + gx(i), H[i][j-1] + gy(j))
+//   sub(i,j) = sum_b rc(i)[b] * cnt(j)[b]   (rc(i)[b] = sum_a cntX(i)[a] c(a,b))
+// Same band / skew / granule machinery as nw_align_affine, plain H in int32.
+// Each cell stores the affine kernels' 4-bit code with both "opened" bits
+// set (a linear gap is always a fresh gap), so trace_pair_affine walks it
+// unchanged: 'D', 'u' (X column vs a gap column), 'l' (gap column vs Y).
+// ===========================================================================
+__global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
+  constexpr int W = 4, SPD = 8;
+  __shared__ __attribute__((aligned(16))) int ring_all[4][128];
+  __shared__ __attribute__((aligned(16))) int4 cwin_all[4][2][256];  // 128 columns x 8 ints, two slots
+  __shared__ __attribute__((aligned(16))) TbLds<W> tbl[4];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  int* ring = ring_all[wid];
+  unsigned* prog = a.prog ? a.prog + blockIdx.x * 4 + wid : nullptr;
+
+  for (;;) {
+    unsigned tk = 0;
+    if (lane == 0) tk = atomicAdd(a.counter, 1u);
+    tk = __builtin_amdgcn_readfirstlane(tk);
+    PROG(0x10000000u | (tk & 0xffffffu));
+    if (tk >= (unsigned)a.ntasks) return;
+    if (__hip_atomic_load((gu32*)a.err, RLX_AGENT) != 0u) return;
+    const int2 task = a.tasks[tk];
+    const PairDesc pd = a.pairs[task.x];
+    const int band = task.y;
+    const int row0 = band * kBandRows + lane * kRows;  // 0-based first DP row of this lane
+    int rc[kRows][kProfSyms], gx[kRows], h[kRows];
+    unsigned acc[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      const int row = min(row0 + r, pd.m - 1);  // rows past m: copies of the last (never traced)
+      const int4* pr = reinterpret_cast<const int4*>(a.prow + (pd.x_off + row) * 8);
+      const int4 q0 = pr[0], q1 = pr[1];
+      rc[r][0] = q0.x; rc[r][1] = q0.y; rc[r][2] = q0.z; rc[r][3] = q0.w; rc[r][4] = q1.x; rc[r][5] = q1.y;
+      gx[r] = q1.z;
+      h[r] = q1.w;  // H[i][0]
+      acc[r] = 0;
+    }
+    int Up = band == 0 ? 0 : a.prow[(pd.x_off + band * kBandRows - 1) * 8 + 7];  // H[row above the band][0]
+    int stH = 0;
+    const bool from_above = band > 0;
+    const bool to_below = band + 1 < pd.nbands;
+    const int64_t bstride = (int64_t)pd.nchunks * 64;
+    const u64* gin = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)(band > 0 ? band - 1 : 0) * bstride + lane;
+    const int last_chunk = pd.nchunks > 0 ? pd.nchunks - 1 : 0;
+    u64* gout = a.bnd + pd.bnd_off + (int64_t)band * bstride + lane;
+    unsigned* mptr = a.mat + pd.mat_off + (int64_t)band * band_dwords(W, pd.sblocks) + lane;
+    // column j (1-based; 0 = the H[0][0] entry) is pcol entry y_off + j; window of sb: columns 64sb-63 .. 64sb+64
+    const int4* colg = reinterpret_cast<const int4*>(a.pcol) + 2 * (pd.y_off - 63);
+    // Granule prefetches are ordinary (compiler-tracked) loads here: this
+    // kernel's register pressure makes the compiler move values between
+    // registers, and a copy of an asm load's destination taken before its
+    // s_waitcnt would read the register before the data landed.
+    u64 pend = from_above ? ld_granule(gin) : 0;
+    bool ok = true;
+
+    for (int sb = 0; sb < pd.sblocks; ++sb) {
+      int bval;  // band-above row: H[row above][64sb + 1 + lane]
+      if (from_above) {
+        bval = 0;
+        if (sb < pd.nchunks) {
+          if (!__all((unsigned)(pend >> 32) == a.epoch)) pend = wait_granules(gin + 64 * sb, a.epoch, pend, a.err);
+          if (!__all((unsigned)(pend >> 32) == a.epoch)) { ok = false; break; }
+          bval = (int)(unsigned)pend;
+        }
+        pend = ld_granule(gin + 64 * min(sb + 1, last_chunk));  // next chunk, used at the next super-block
+      } else {
+        bval = a.pcol[(pd.y_off + 64 * sb + lane + 1) * 8 + 7];  // H[0][j]
+      }
+      int* slot = ring + (sb & 1) * 64;
+      slot[lane] = bval;
+      int4* cw = cwin_all[wid][sb & 1];
+      // columns 64sb-63 .. 64sb+64: 128 entries of 8 ints = 256 int4
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cw[lane + 64 * k] = colg[128 * sb + lane + 64 * k];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      for (int blk = 0; blk < 8; ++blk) {
+        const int s0 = sb * 64 + blk * 8;
+        const int4 bA = *reinterpret_cast<const int4*>(slot + blk * 8);
+        const int4 bB = *reinterpret_cast<const int4*>(slot + blk * 8 + 4);
+        const int bv[8] = {bA.x, bA.y, bA.z, bA.w, bB.x, bB.y, bB.z, bB.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          stH = __builtin_amdgcn_update_dpp(h[kRows - 1], stH, 0x130 /*wave_shl:1*/, 0xf, 0xf, false);
+          const int uh = __builtin_amdgcn_update_dpp(bv[k], h[kRows - 1], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
+          const int dg0 = Up;
+          Up = uh;
+          // this lane's column j = s - lane + 1 -> window entry j - (64sb - 63) = (s - 64sb) - lane + 64
+          const int we = blk * 8 + k - lane + 64;
+          const int4 c0 = cw[2 * we], c1 = cw[2 * we + 1];
+          const int cy[kProfSyms] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y};
+          const int gy = c1.z;
+          const bool valid = (s0 + k) >= lane;  // column >= 1; else the border H[i][0] stays
+          int nh[kRows], hp = uh;
+#pragma unroll
+          for (int r = 0; r < kRows; ++r) {
+            int sub = 0;
+#pragma unroll
+            for (int b = 0; b < kProfSyms; ++b) sub += (int)__umul24((unsigned)rc[r][b], (unsigned)cy[b]);
+            const int d = (r ? h[r - 1] : dg0) + sub;  // diag: row above, previous step
+            const int u = hp + gx[r];                   // up: row above, this step
+            const int l = h[r] + gy;                    // left: this row, previous step
+            const int hv = min(min(d, u), l);
+            const unsigned code = (d == hv ? 0u : (u == hv ? 1u : 2u)) | 12u;
+            acc[r] = __builtin_amdgcn_alignbit(code, acc[r], 4);
+            nh[r] = valid ? hv : h[r];
+            hp = nh[r];
+          }
+#pragma unroll
+          for (int r = 0; r < kRows; ++r) h[r] = nh[r];
+          if (k == 7) {
+#pragma unroll
+            for (int r = 0; r < kRows; ++r) __builtin_nontemporal_store(acc[r], mptr + r * kWave);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        mptr += (8 / SPD) * kRows * kWave;
+      }
+      if (to_below && sb >= 1 && sb <= pd.nchunks) st_granule(gout + 64 * (sb - 1), a.epoch, stH);
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(pend) :: "memory");
+      __builtin_amdgcn_wave_barrier();
+      PROG(0x20000000u | ((unsigned)band << 12) | (unsigned)(sb & 0xfff));
+    }
+    if (!ok) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PROG(0x30000000u);
+    unsigned prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add((gu32*)(a.done + pd.slot), 1u, RLX_AGENT);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev + 1u == (unsigned)pd.nbands) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      PROG(0x40000000u);
+      trace_pair_affine(a, pd, tbl[wid], lane, prog);
+      PROG(0x60000000u);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 template <int MODE, int W>
 static hipError_t fill_w(const FillArgs& a, int grid, hipStream_t s) {
@@ -1758,6 +1905,10 @@ hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStrea
       if (bits != 4) return hipErrorInvalidValue;
       hipLaunchKernelGGL(nw_align_pk2, dim3(grid), dim3(256), 0, s, a);
       return hipGetLastError();
+    case kProfileDP:
+      if (bits != 4) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(nw_profile, dim3(grid), dim3(256), 0, s, a);
+      return hipGetLastError();
     case kProfile: return fill_m<kProfile>(bits, a, grid, s);
     case kCompare: return fill_m<kCompare>(bits, a, grid, s);
     case kLiteral: return bits == 32 ? fill_w<kLiteral, 32>(a, grid, s) : hipErrorInvalidValue;
@@ -1775,11 +1926,12 @@ static int occ_w() {
 
 int fill_blocks_per_cu(int mode, int bits) {
   if (mode == kLiteral) return occ_w<kLiteral, 32>();
-  if (mode == kAffine || mode == kPacked || mode == kPacked2) {
+  if (mode == kAffine || mode == kPacked || mode == kPacked2 || mode == kProfileDP) {
     int n = 0;
-    const void* f = mode == kAffine   ? reinterpret_cast<const void*>(&nw_align_affine)
-                    : mode == kPacked ? reinterpret_cast<const void*>(&nw_align_pk)
-                                      : reinterpret_cast<const void*>(&nw_align_pk2);
+    const void* f = mode == kAffine     ? reinterpret_cast<const void*>(&nw_align_affine)
+                    : mode == kPacked   ? reinterpret_cast<const void*>(&nw_align_pk)
+                    : mode == kPacked2  ? reinterpret_cast<const void*>(&nw_align_pk2)
+                                        : reinterpret_cast<const void*>(&nw_profile);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 256, 0) != hipSuccess) return 1;
     return n > 0 ? n : 1;
   }

@@ -155,6 +155,7 @@ struct nwk_ctx {
   DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij, d_done, d_stamps, d_prog;
   DevBuf d_segctl;              // kPacked2: task-done flags | segment info | traceback records
   DevBuf d_pen, d_hash;         // device finalize (nw_hash): per pair penalty, problemhash
+  DevBuf d_msa[3];              // nwk_msa: row profiles | column profiles | granules, matrices, moves
   HostBuf h_pen[2], h_hash[2];
   bool has_us = false;          // some input byte is '_': trims need the host finalize
   HostBuf h_tasks;
@@ -189,6 +190,7 @@ void nwk_ctx_destroy(nwk_ctx* c) {
   c->d_pairs.release(); c->d_tasks.release(); c->d_ctl.release();
   c->d_oplen.release(); c->d_endij.release(); c->d_done.release(); c->d_stamps.release();
   c->d_segctl.release(); c->d_prog.release(); c->d_pen.release(); c->d_hash.release();
+  for (auto& b : c->d_msa) b.release();
   for (int b = 0; b < 2; ++b) { c->h_pen[b].release(); c->h_hash[b].release(); }
   c->h_tasks.release();
   for (int b = 0; b < 2; ++b) {
@@ -1304,6 +1306,294 @@ static int min_penalties_sc(const uint8_t* seqs, const int64_t* offsets, int32_t
   for (int64_t p = 0; p < P; ++p)
     if (!have[p]) return fail(NWK_ECOMM, "pair %lld missing after all-gather", (long long)p);
   return nwk_chain_hash(ph.data(), P, hash_hex);
+}
+
+// ---------------------------------------------------------------------------
+// Progressive sum-of-pairs MSA (build-defined, oracle
+// oracle/msa_oracle.c nwo_msa): UPGMA on the pairwise penalties, then one
+// profile-profile DP per merge on the GPU (nw_profile + the fused affine-code
+// traceback), merges of independent subtrees batched into one launch.
+// ---------------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+
+struct Prof {
+  std::vector<uint8_t> rows;  // nseq x len, row-major ('_' = gap)
+  std::vector<int> members;   // input sequence index of each row
+  int len = 0;
+};
+
+inline int64_t sym_cost(int a, int b, int gap, int pxy, int pgap) {
+  if (a == gap || b == gap) return (a == gap && b == gap) ? 0 : pgap;
+  return a == b ? 0 : pxy;
+}
+
+// Column symbol counts of a profile (S symbols, the last = gap).
+void prof_counts(const Prof& P, const uint8_t* code_of, int S, std::vector<int>* cnt) {
+  const int n = (int)P.members.size();
+  cnt->assign((size_t)P.len * S, 0);
+  for (int r = 0; r < n; ++r)
+    for (int i = 0; i < P.len; ++i) {
+      const uint8_t ch = P.rows[(size_t)r * P.len + i];
+      (*cnt)[(size_t)i * S + (ch == '_' ? S - 1 : code_of[ch])]++;
+    }
+}
+
+// NWK_WATCHDOG=<s> debug: report the wave markers of a launch that does not finish, then exit.
+void watchdog_wait(nwk_ctx* c, const unsigned* prog, int grid) {
+  static const int watchdog = getenv("NWK_WATCHDOG") ? atoi(getenv("NWK_WATCHDOG")) : 0;
+  if (watchdog <= 0 || !prog) return;
+  const double t0 = now_ms();
+  while (hipStreamQuery(c->stream) == hipErrorNotReady && now_ms() - t0 < watchdog * 1000.0) usleep(10000);
+  if (hipStreamQuery(c->stream) != hipErrorNotReady) return;
+  std::vector<unsigned> pg(4 * (size_t)(grid + 1));
+  hipStream_t s2;
+  (void)hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+  (void)hipMemcpyAsync(pg.data(), prog, 4 * pg.size(), hipMemcpyDeviceToHost, s2);
+  (void)hipStreamSynchronize(s2);
+  fprintf(stderr, "nwk watchdog: launch still running after %d s; wave markers:\n", watchdog);
+  for (size_t q = 0; q < pg.size(); ++q)
+    if (pg[q]) fprintf(stderr, "  wave %zu: %08x\n", q, pg[q]);
+  fflush(stderr);
+  _exit(3);
+}
+
+}  // namespace
+
+extern "C" {
+
+int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uint8_t* rows, int64_t cap,
+            int64_t* len, int64_t* sop) {
+  if (!c || !len || !sop || (c->k > 1 && !penalties) || (c->k > 0 && !rows)) return fail(NWK_EINVAL, "nwk_msa: bad argument");
+  if (pxy < 0 || pgap < 0) return fail(NWK_EINVAL, "nwk_msa: penalties must be >= 0");
+  if (c->has_us) return fail(NWK_EINVAL, "nwk_msa: '_' is the gap symbol and may not occur in the input");
+  const int k = c->k, S = c->alpha + 1, gap = S - 1;
+  if (S > kProfSyms) return fail(NWK_EINVAL, "nwk_msa: %d distinct input bytes (at most %d)", c->alpha, kProfSyms - 1);
+  *len = 0;
+  *sop = 0;
+  if (k == 0) return NWK_OK;
+  const int nc = 2 * k - 1;
+  std::vector<Prof> prof((size_t)nc);
+  for (int s = 0; s < k; ++s) {
+    prof[s].len = (int)(c->off[s + 1] - c->off[s]);
+    prof[s].rows.assign(c->seqs.begin() + c->off[s], c->seqs.begin() + c->off[s + 1]);
+    prof[s].members = {s};
+  }
+  // ---- UPGMA (oracle nwo_msa): mean pairwise penalty, exact ratio compare, ties -> smallest ids
+  std::vector<int64_t> Ssum((size_t)nc * nc, 0);
+  std::vector<int> sz((size_t)nc, 0), round_of((size_t)nc, 0);
+  std::vector<char> alive((size_t)nc, 0);
+  for (int s = 0; s < k; ++s) sz[s] = 1, alive[s] = 1;
+  for (int i = 1; i < k; ++i)
+    for (int j = 0; j < i; ++j) Ssum[(size_t)i * nc + j] = Ssum[(size_t)j * nc + i] = penalties[(int64_t)i * (i - 1) / 2 + j];
+  struct Merge { int x, y, id; };
+  std::vector<Merge> merges;
+  for (int nid = k; nid < nc; ++nid) {
+    int ba = -1, bb = -1;
+    for (int a = 0; a < nid; ++a) {
+      if (!alive[a]) continue;
+      for (int b = a + 1; b < nid; ++b) {
+        if (!alive[b]) continue;
+        if (ba < 0) { ba = a; bb = b; continue; }
+        const __int128 lhs = (__int128)Ssum[(size_t)a * nc + b] * sz[ba] * sz[bb];
+        const __int128 rhs = (__int128)Ssum[(size_t)ba * nc + bb] * sz[a] * sz[b];
+        if (lhs < rhs) { ba = a; bb = b; }
+      }
+    }
+    merges.push_back(Merge{bb, ba, nid});  // rows: the younger cluster (skel's x = genes[i], i > j)
+    sz[nid] = sz[ba] + sz[bb];
+    round_of[nid] = 1 + std::max(round_of[ba], round_of[bb]);
+    alive[ba] = alive[bb] = 0;
+    alive[nid] = 1;
+    for (int o = 0; o < nid; ++o)
+      if (alive[o]) Ssum[(size_t)nid * nc + o] = Ssum[(size_t)o * nc + nid] = Ssum[(size_t)ba * nc + o] + Ssum[(size_t)bb * nc + o];
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  const int max_round = k > 1 ? round_of[nc - 1] : 0;
+  DevBuf &d_prow = c->d_msa[0], &d_pcol = c->d_msa[1], &d_mw = c->d_msa[2], &d_pd = c->d_pairs, &d_tk = c->d_tasks;
+  for (int rd = 1; rd <= max_round; ++rd) {
+    std::vector<Merge> ms;
+    for (const auto& m : merges)
+      if (round_of[m.id] == rd) ms.push_back(m);
+    const int np = (int)ms.size();
+    // ---- profile arrays: X columns (DP rows) {rc[0..5], gx, H[i][0]}, Y columns {cnt[0..5], gy, H[0][j]}
+    std::vector<int> hrow, hcol;
+    std::vector<PairDesc> pd((size_t)np);
+    std::vector<std::vector<int>> cy_host((size_t)np), rc_host((size_t)np);
+    int64_t mat = 0, bnd = 0, ops = 0, ntasks = 0;
+    for (int q = 0; q < np; ++q) {
+      const Prof &X = prof[ms[q].x], &Y = prof[ms[q].y];
+      const int nx = (int)X.members.size(), ny = (int)Y.members.size(), LX = X.len, LY = Y.len;
+      std::vector<int> cx, cyv;
+      prof_counts(X, c->code_of, S, &cx);
+      prof_counts(Y, c->code_of, S, &cyv);
+      int64_t maxstep = 0, acc = 0;
+      const int64_t xoff = (int64_t)hrow.size() / 8;
+      std::vector<int>& rch = rc_host[q];
+      rch.assign((size_t)LX * 8, 0);
+      for (int i = 0; i < LX; ++i) {
+        int64_t rcb[kProfSyms] = {0};
+        for (int b = 0; b < S; ++b)
+          for (int a2 = 0; a2 < S; ++a2) rcb[b] += (int64_t)cx[(size_t)i * S + a2] * sym_cost(a2, b, gap, pxy, pgap);
+        const int64_t gx = (int64_t)(nx - cx[(size_t)i * S + gap]) * ny * pgap;
+        acc += gx;
+        for (int b = 0; b < kProfSyms; ++b) rch[(size_t)i * 8 + b] = (int)(b < S ? rcb[b] : 0);
+        rch[(size_t)i * 8 + 6] = (int)gx;
+        rch[(size_t)i * 8 + 7] = (int)acc;
+        int64_t mx = gx;
+        for (int b = 0; b < S; ++b) mx = std::max(mx, rcb[b] * ny);
+        maxstep = std::max(maxstep, mx);
+        if (mx >= (1 << 24)) return fail(NWK_EINVAL, "nwk_msa: profile costs exceed the kernel's 24-bit products");
+      }
+      hrow.insert(hrow.end(), rch.begin(), rch.end());
+      // columns: entry y_off + j holds column j (j = 0: H[0][0] = 0), 64 pad entries before, 192 after
+      const int64_t yoff = (int64_t)hcol.size() / 8 + 64;
+      std::vector<int> colv((size_t)(LY + 64 + 192) * 8, 0);
+      int64_t accy = 0;
+      for (int j = 1; j <= LY; ++j) {
+        int* e = &colv[(size_t)(64 + j) * 8];
+        for (int b = 0; b < S; ++b) e[b] = cyv[(size_t)(j - 1) * S + b];
+        const int64_t gy = (int64_t)(ny - cyv[(size_t)(j - 1) * S + gap]) * nx * pgap;
+        accy += gy;
+        e[6] = (int)gy;
+        e[7] = (int)accy;
+        maxstep = std::max(maxstep, gy);
+      }
+      for (int j = LY + 1; j < LY + 192; ++j) colv[(size_t)(64 + j) * 8 + 7] = (int)accy;  // (never traced)
+      cy_host[q] = cyv;
+      hcol.insert(hcol.end(), colv.begin(), colv.end());
+      if ((int64_t)(LX + LY + 2) * maxstep + acc + accy >= (1ll << 30))
+        return fail(NWK_EINVAL, "nwk_msa: profile DP of %d x %d columns would exceed int32", LX, LY);
+      PairDesc& d = pd[q];
+      memset(&d, 0, sizeof d);
+      d.x_off = xoff;
+      d.y_off = yoff;
+      d.m = LX;
+      d.n = LY;
+      d.nbands = (int)ceil_div(LX, kBandRows);
+      d.nchunks = (int)ceil_div(LY, 64);
+      d.sblocks = d.nchunks + 1;
+      d.slot = q;
+      d.mat_off = mat;
+      d.bnd_off = bnd;
+      d.ops_off = ops;
+      mat += (int64_t)d.nbands * band_dwords(4, d.sblocks);
+      bnd += (int64_t)d.nbands * d.nchunks * 64;  // granules of each band's last row (the last band's unused)
+      ops += round_up((int64_t)LX + LY, 16);
+      ntasks += d.nbands;
+    }
+    // ---- device buffers: [granules | matrices | ops]
+    const int64_t bnd_b = round_up(bnd * 8 + 4096, 256), mat_b = round_up(mat * 4, 256);
+    const int64_t work_b = bnd_b + mat_b + ops + 4096;
+    if ((rc = d_mw.ensure((size_t)work_b)) != NWK_OK) return rc;
+    if ((rc = d_prow.ensure(4 * hrow.size() + 64)) != NWK_OK) return rc;
+    if ((rc = d_pcol.ensure(4 * hcol.size() + 64)) != NWK_OK) return rc;
+    if ((rc = d_pd.ensure(sizeof(PairDesc) * np)) != NWK_OK) return rc;
+    if ((rc = d_tk.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
+    std::vector<int2> tk;
+    for (int q = 0; q < np; ++q)
+      for (int b = 0; b < pd[q].nbands; ++b) tk.push_back(make_int2(q, b));
+    for (auto& d : pd) { d.mat_off += bnd_b / 4; d.ops_off += bnd_b + mat_b; }
+    if ((rc = c->d_oplen.ensure(sizeof(int) * np)) != NWK_OK) return rc;
+    if ((rc = c->d_endij.ensure(sizeof(int2) * np)) != NWK_OK) return rc;
+    if ((rc = c->d_done.ensure(sizeof(unsigned) * np)) != NWK_OK) return rc;
+    HIP_TRY(hipMemsetAsync(d_mw.p, 0, (size_t)bnd_b, c->stream));  // granule tags start below any epoch
+    HIP_TRY(hipMemcpyAsync(d_prow.p, hrow.data(), 4 * hrow.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_pcol.p, hcol.data(), 4 * hcol.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_pd.p, pd.data(), sizeof(PairDesc) * np, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_tk.p, tk.data(), sizeof(int2) * ntasks, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_ctl.p, 0, 256, c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_done.p, 0, sizeof(unsigned) * np, c->stream));
+    FillArgs fa;
+    memset(&fa, 0, sizeof fa);
+    fa.pairs = d_pd.as<PairDesc>();
+    fa.tasks = d_tk.as<int2>();
+    fa.ntasks = (int)ntasks;
+    fa.mat = d_mw.as<uint32_t>();
+    fa.bnd = d_mw.as<unsigned long long>();
+    fa.counter = c->d_ctl.as<unsigned>();
+    fa.err = c->d_ctl.as<unsigned>() + 16;
+    fa.done = c->d_done.as<unsigned>();
+    fa.ops = d_mw.as<uint8_t>();
+    fa.oplen = c->d_oplen.as<int>();
+    fa.endij = c->d_endij.as<int2>();
+    fa.epoch = 1;
+    fa.ntasks_pairs = np;
+    fa.prow = d_prow.as<int>();
+    fa.pcol = d_pcol.as<int>();
+    const int grid = (int)std::min<int64_t>(fill_blocks_per_cu(kProfileDP, 4) * c->cus, ceil_div(ntasks, 4));
+    if (getenv("NWK_WATCHDOG")) {
+      if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;
+      HIP_TRY(hipMemsetAsync(c->d_prog.p, 0, 4 * (size_t)(grid + 1) * 4, c->stream));
+      fa.prog = c->d_prog.as<unsigned>();
+    }
+    if (c->opts.verbose >= 3) {
+      fprintf(stderr, "nwk_msa round %d: %d merges, %lld band tasks, grid %d\n", rd, np, (long long)ntasks, grid);
+      fflush(stderr);
+    }
+    HIP_TRY(launch_fill(kProfileDP, 4, fa, grid, c->stream));
+    watchdog_wait(c, fa.prog, grid);
+    std::vector<int> ol((size_t)np);
+    std::vector<int2> ej((size_t)np);
+    std::vector<uint8_t> hops((size_t)ops);
+    unsigned herr = 0;
+    HIP_TRY(hipMemcpyAsync(&herr, fa.err, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(ol.data(), fa.oplen, 4 * np, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(ej.data(), fa.endij, 8 * np, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(hops.data(), d_mw.as<uint8_t>() + bnd_b + mat_b, (size_t)ops, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (herr) return fail(NWK_EKERNEL, "nwk_msa: profile kernel fault (err=%u)", herr);
+    // ---- merged profiles and merge costs (forward moves: prefix run, then the reversed trace)
+    for (int q = 0; q < np; ++q) {
+      const Prof &X = prof[ms[q].x], &Y = prof[ms[q].y];
+      const int nx = (int)X.members.size(), ny = (int)Y.members.size();
+      std::string mv;
+      const int ei = ej[q].x, ejj = ej[q].y;
+      if (ol[q] < 0 || ol[q] > X.len + Y.len || ei < 0 || ei > X.len || ejj < 0 || ejj > Y.len || (ei && ejj))
+        return fail(NWK_EKERNEL, "nwk_msa: bad traceback (len %d, end %d,%d) for %d x %d", ol[q], ei, ejj, X.len, Y.len);
+      mv.append((size_t)ei, 'U');
+      mv.append((size_t)ejj, 'L');
+      const uint8_t* o = hops.data() + (pd[q].ops_off - bnd_b - mat_b);
+      for (int t = ol[q] - 1; t >= 0; --t) mv.push_back(o[t] == 'D' ? 'D' : (o[t] == 'u' || o[t] == 'U') ? 'U' : 'L');
+      Prof& N = prof[ms[q].id];
+      N.len = (int)mv.size();
+      N.members = X.members;
+      N.members.insert(N.members.end(), Y.members.begin(), Y.members.end());
+      N.rows.assign((size_t)(nx + ny) * N.len, '_');
+      int64_t cost = 0;
+      int i = 0, j = 0;
+      const std::vector<int>& rch = rc_host[q];
+      const std::vector<int>& cyv = cy_host[q];
+      for (int t = 0; t < N.len; ++t) {
+        const char m = mv[(size_t)t];
+        if ((m != 'L' && i >= X.len) || (m != 'U' && j >= Y.len))
+          return fail(NWK_EKERNEL, "nwk_msa: traced path leaves the %d x %d matrix", X.len, Y.len);
+        if (m != 'L') for (int r = 0; r < nx; ++r) N.rows[(size_t)r * N.len + t] = X.rows[(size_t)r * X.len + i];
+        if (m != 'U') for (int r = 0; r < ny; ++r) N.rows[(size_t)(nx + r) * N.len + t] = Y.rows[(size_t)r * Y.len + j];
+        if (m == 'D') {
+          for (int b = 0; b < S; ++b) cost += (int64_t)rch[(size_t)i * 8 + b] * cyv[(size_t)j * S + b];
+        } else if (m == 'U') {
+          cost += rch[(size_t)i * 8 + 6];
+        } else {
+          cost += (int64_t)(ny - cyv[(size_t)j * S + gap]) * nx * pgap;
+        }
+        i += m != 'L';
+        j += m != 'U';
+      }
+      if (i != X.len || j != Y.len) return fail(NWK_EKERNEL, "nwk_msa: traced path ends at (%d, %d) of (%d, %d)", i, j, X.len, Y.len);
+      *sop += cost;
+      prof[ms[q].x] = Prof();
+      prof[ms[q].y] = Prof();
+    }
+  }
+  const Prof& R = prof[nc - 1];
+  if (R.len > cap) return fail(NWK_EINVAL, "nwk_msa: MSA length %d exceeds cap %lld", R.len, (long long)cap);
+  *len = R.len;
+  for (size_t r = 0; r < R.members.size(); ++r)
+    memcpy(rows + (size_t)R.members[r] * cap, R.rows.data() + r * R.len, (size_t)R.len);
+  return NWK_OK;
 }
 
 int nwk_get_minimum_penalties(const uint8_t* seqs, const int64_t* offsets, int32_t k, int32_t pxy, int32_t pgap,

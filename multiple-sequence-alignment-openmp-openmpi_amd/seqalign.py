@@ -66,6 +66,7 @@ SIGNATURES = {
     "nwk_align_all_affine": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P, _P]),
     "nwk_get_minimum_penalty_affine": (ctypes.c_int, [_P, _P, _I32, _P, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),
     "nwk_get_minimum_penalties_affine": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P]),
+    "nwk_msa": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _I64, _P, _P]),
     "nwk_shard_pairs": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
     "nwk_chain_hash": (ctypes.c_int, [_P, _I64, _P]),
     "nwk_sha512_hex": (None, [_P, _I64, _P]),
@@ -235,6 +236,20 @@ class Engine:
                                                 ctypes.byref(alen), ctypes.byref(pen)))
         self.k = 2
         return pen.value, a1.raw[:alen.value], a2.raw[:alen.value]
+
+    def msa(self, pxy, pgap, penalties=None):
+        """Progressive sum-of-pairs MSA of the current set (nwk_msa):
+        returns (rows: list of k bytes, '_' = gap, SoP score).  penalties: the
+        pairwise penalties in canonical order (computed with align_all when None)."""
+        if penalties is None:
+            penalties = self.align_all(pxy, pgap)[1] if self.k > 1 else np.zeros(0, np.int32)
+        pen = np.ascontiguousarray(penalties, dtype=np.int32)
+        cap = max(int(self._offs[-1]) if self._offs is not None else 0, 1)
+        rows = np.zeros((max(self.k, 1), cap), dtype=np.uint8)
+        ln, sop = ctypes.c_int64(), ctypes.c_int64()
+        _check(self.lib.nwk_msa(self._ctx, pxy, pgap, _ptr(pen) if pen.size else None, _ptr(rows), cap,
+                                ctypes.byref(ln), ctypes.byref(sop)))
+        return [bytes(rows[r, :ln.value]) for r in range(self.k)], sop.value
 
 
 def chain_hash(problem_hashes):

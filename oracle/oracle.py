@@ -127,6 +127,46 @@ def all_pairs(genes, pxy, pgap):
     return out.value.decode(), [int(v) for v in pen[:P]], [raw[128 * p:128 * p + 128].decode() for p in range(P)]
 
 
+def profile_align(X, Y, pxy, pgap):
+    """Profile-profile NW (msa_oracle.c): X, Y lists of equal-length rows -> (cost, ops 'D'/'U'/'L')."""
+    X, Y = [_b(r) for r in X], [_b(r) for r in Y]
+    lx, ly = len(X[0]), len(Y[0])
+    ops = ctypes.create_string_buffer(lx + ly + 1)
+    n = ctypes.c_int()
+    lib().nwo_profile_align.restype = ctypes.c_longlong
+    c = lib().nwo_profile_align(b"".join(X), len(X), lx, b"".join(Y), len(Y), ly, pxy, pgap, ops, ctypes.byref(n))
+    return c, ops.raw[:n.value].decode()
+
+
+def sop(rows, pxy, pgap):
+    """Sum-of-pairs score of equal-length rows."""
+    rows = [_b(r) for r in rows]
+    lib().nwo_sop.restype = ctypes.c_longlong
+    return lib().nwo_sop(b"".join(rows), len(rows), len(rows[0]) if rows else 0, pxy, pgap)
+
+
+def msa(genes, pxy, pgap, penalties=None):
+    """Progressive SoP MSA (build-defined): (rows in input order, SoP score)."""
+    bs = [_b(g) for g in genes]
+    k = len(bs)
+    if penalties is None:
+        penalties = all_pairs(bs, pxy, pgap)[1]
+    offs = np.zeros(k + 1, dtype=np.int64)
+    if k:
+        offs[1:] = np.cumsum([len(b) for b in bs])
+    cap = max(1, int(offs[-1]))
+    rows = ctypes.create_string_buffer(max(k, 1) * cap)
+    pen = np.array(list(penalties) or [0], dtype=np.int32)
+    ln = ctypes.c_int()
+    sp = ctypes.c_longlong()
+    rc = lib().nwo_msa(b"".join(bs) or b"\0", offs.ctypes.data_as(ctypes.c_void_p), k, pxy, pgap,
+                       pen.ctypes.data_as(ctypes.c_void_p), rows, cap, ctypes.byref(ln), ctypes.byref(sp))
+    if rc != 0:
+        raise MemoryError("oracle: msa failed")
+    raw = rows.raw
+    return [raw[r * cap:r * cap + ln.value] for r in range(k)], sp.value
+
+
 def run_cli(exe, text, timeout=3600, env=None):
     """Runs a program with the reference's stdin/stdout contract.
     Returns (time_us, hash, penalties)."""

@@ -346,3 +346,56 @@ def test_driver_fasta_and_dump(golden, tmp_path):
             assert lines[3 * p] == b"%d %d %d" % (i, j, pen)
             assert lines[3 * p + 1] == a1 and lines[3 * p + 2] == a2
             p += 1
+
+
+# --- progressive SoP MSA (build-defined; oracle/msa_oracle.c nwo_msa)
+
+MSA_K2 = [c for c in GOLDEN if len(case_input(c)[2]) == 2 and min(case_input(c)[:2]) >= 0
+          and b"_" not in b"".join(case_input(c)[2])]
+
+
+@pytest.mark.parametrize("case", MSA_K2, ids=[c["name"] for c in MSA_K2])
+def test_msa_k2_golden(engine, case):
+    """k = 2: the MSA is the reference's alignment of pair (1, 0) and its SoP the golden penalty."""
+    pxy, pgap, genes = case_input(case)
+    engine.set_sequences(genes)
+    rows, s = engine.msa(pxy, pgap)
+    assert s == case["penalties"][0]
+    assert (rows, s) == oracle.msa(genes, pxy, pgap)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_msa_random_vs_oracle(engine, seed):
+    r = random.Random(500 + seed)
+    alpha = [b"ACGT", b"AC", b"ACGTN"][seed % 3]
+    pxy, pgap = [(3, 2), (5, 1), (1, 3), (0, 2), (4, 0), (7, 7), (2, 1), (9, 4)][seed]
+    k = r.randint(3, 9)
+    if seed % 2:
+        genes = _mutants(r, _rand_genes(r, 1, 200, 1400, alpha)[0], k, alpha)
+    else:
+        genes = _rand_genes(r, k, 1, 1300, alpha)
+    genes = [g or alpha[:1] for g in genes]
+    engine.set_sequences(genes)
+    rows, s = engine.msa(pxy, pgap)
+    want_rows, want_s = oracle.msa(genes, pxy, pgap)
+    assert s == want_s
+    assert rows == want_rows
+    assert oracle.sop(rows, pxy, pgap) == s
+
+
+def test_msa_small_and_edge_sets(engine):
+    for genes in ([b"ACGT"], [b"A", b"A"], [b"A", b"C"], [b"AC", b"A", b"C", b"CA"], [b"A" * 600, b"C"]):
+        engine.set_sequences(genes)
+        assert engine.msa(3, 2) == oracle.msa(genes, 3, 2)
+
+
+def test_msa_rejects_what_it_cannot_align(engine):
+    engine.set_sequences([b"AC_G", b"ACG"])
+    with pytest.raises(seqalign.NwkError):
+        engine.msa(3, 2)
+    engine.set_sequences([b"ACG", b"AG"])
+    with pytest.raises(seqalign.NwkError):
+        engine.msa(-1, 2)
+    engine.set_sequences([b"ABCDEF", b"AB"])
+    with pytest.raises(seqalign.NwkError):
+        engine.msa(3, 2)
