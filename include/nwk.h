@@ -58,7 +58,9 @@ typedef struct nwk_opts {
   int64_t workspace_bytes;   /* HBM budget per device; 0 = 92% of free memory */
   int32_t verbose;           /* 1 = per-call statistics on stderr */
   int32_t finalize;          /* pair finalize (rows, penalty, SHA-512): 0 auto, 1 host, 2 device (nw_hash) */
-  int32_t reserved[4];
+  int32_t linear_space;      /* linear-space traceback: 0 = only for pairs whose matrix exceeds
+                                the HBM budget, -1 = never, G > 0 = every pair, G bands per recompute group */
+  int32_t reserved[3];
 } nwk_opts;
 
 typedef struct nwk_stats {
@@ -72,7 +74,8 @@ typedef struct nwk_stats {
   int32_t mode;              /* 0 = profile, 1 = compare, 2 = literal, 3 = affine, 4 = packed profile, 5 = packed band pairs */
   int32_t fill_launches;     /* fill-kernel launches in the call */
   int32_t device_finalized;  /* batches whose pairs were finalized on the device */
-  int32_t reserved[3];
+  int32_t linear_space_pairs; /* pairs aligned with the linear-space traceback */
+  int32_t reserved[2];
 } nwk_stats;
 
 /* Defaults for nwk_opts (device 0, auto everything). */

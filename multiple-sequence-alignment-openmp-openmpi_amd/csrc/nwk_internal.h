@@ -48,6 +48,9 @@ struct PairDesc {
   int64_t seg_off;      // first entry of this pair in seginfo (tasks * nguess)
   int64_t rec_off;      // first record of this pair in recs ([m / 128 + 1][2])
   int64_t segops_off;   // first byte of this pair's segment move buffers in segops
+  // linear-space traceback group (FillArgs.lin_mode 2): bands in the group,
+  // trace start cell, row where the trace stops (the group's top)
+  int32_t lin_nb, lin_i, lin_j, lin_stop;
 };
 
 struct FillArgs {
@@ -71,6 +74,7 @@ struct FillArgs {
   int K0, K1;              // diag increments in G-space: match, mismatch (kAffine: K1 = pxy)
   int go, ge;              // kAffine: gap open / extend
   int dbg_notrace;         // debug: skip the affine traceback
+  int lin_mode;            // nw_align: 0 normal, 1 linear-space fill pass, 2 linear-space group recompute + trace
   unsigned* prog;          // debug: per-wave progress markers (NWK_WATCHDOG)
   unsigned* tdone;         // kPacked2: per task, 1 = filled and released
   int* seginfo;            // kPacked2: per task, 8 ints {len, ei, ej, mseg, midx, off lo, off hi, -}

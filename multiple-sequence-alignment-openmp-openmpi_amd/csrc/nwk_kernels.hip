@@ -133,7 +133,7 @@ template <int MODE, int W, bool MASK>
 __device__ __forceinline__ void step_block(int s0, int lane, int (&h)[kRows], int& Up, int& stage,
                                            unsigned (&acc)[kRows], const unsigned (&xq)[kRows],
                                            unsigned e0, unsigned e1, const int* bslot,
-                                           unsigned* mptr, int K0, int K1) {
+                                           unsigned* mptr, int K0, int K1, bool store = true) {
   constexpr int SPD = 32 / W;
   const int4 bA = *reinterpret_cast<const int4*>(bslot);
   const int4 bB = *reinterpret_cast<const int4*>(bslot + 4);
@@ -165,7 +165,7 @@ __device__ __forceinline__ void step_block(int s0, int lane, int (&h)[kRows], in
 #pragma unroll
       for (int r = 0; r < kRows; ++r) acc[r] = __builtin_amdgcn_alignbit((unsigned)h[r], acc[r], W);
     }
-    if ((k % SPD) == SPD - 1) {
+    if ((k % SPD) == SPD - 1 && store) {  // (linear-space fill pass: boundary rows only)
 #pragma unroll
       for (int r = 0; r < kRows; ++r)
         __builtin_nontemporal_store(W < 32 ? acc[r] : (unsigned)h[r], mptr + ((k / SPD) * kRows + r) * kWave);
@@ -330,6 +330,7 @@ struct SegCtx {
   const unsigned* tdone;           // per pair task-done flags, nullptr: all done
   int task_shift;                  // band -> task: b >> task_shift
   const unsigned* resolved;        // speculative segments: the pair's chain is complete -> abort (mseg -4)
+  int stop = 0;                    // linear-space groups: the walk ends on entering this row (a band top)
 };
 struct SegOut {
   int len, ei, ej;                 // moves, end cell
@@ -400,7 +401,7 @@ __device__ __forceinline__ SegOut trace_pair(const FillArgs& a, const PairDesc& 
   };
   const int li = lane >> 3, lj = lane & 7;  // this lane's cell: (i - li, j - lj)
 
-  while (i > 0 && j > 0) {
+  while (i > sc.stop && j > 0) {
     if (prof) tA = __builtin_amdgcn_s_memtime();
     if (sc.recs && (i & (kRecRows - 1)) == 0 && i != last_rec) {  // arrived on a record row
       last_rec = i;
@@ -568,7 +569,7 @@ __device__ __forceinline__ SegOut trace_pair(const FillArgs& a, const PairDesc& 
     // lane index, one byte store per step.
     const int nli = li + (isD || isU ? 1 : 0), nlj = lj + (isU ? 0 : 1);
     // (segments) also stop on entering a record row
-    const bool leaves = nli > 7 || nlj > 7 || i - nli <= 0 || j - nlj <= 0 ||
+    const bool leaves = nli > 7 || nlj > 7 || i - nli <= sc.stop || j - nlj <= 0 ||
                         (sc.recs && nli > li && ((i - nli) & (kRecRows - 1)) == 0);
     const unsigned code = (isD ? (unsigned)'D' : isU ? (unsigned)'U' : (unsigned)'L') |
                           ((leaves ? 64u : (unsigned)(nli * 8 + nlj)) << 8);
@@ -648,7 +649,12 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
     }
 
     const bool from_above = band > 0;
-    const bool to_below = band + 1 < pd.nbands;
+    // linear-space traceback (a.lin_mode): 1 = fill pass keeping only the
+    // boundary rows; 2 = recompute of a group of bands from those rows (all
+    // already carry this epoch: no waiting, no publishing) into a scratch
+    // matrix, then the trace through the group
+    const bool store = a.lin_mode != 1;
+    const bool to_below = band + 1 < pd.nbands && a.lin_mode != 2;
     const int64_t bstride = (int64_t)pd.nchunks * 64;
     // band 0 has no band above: its (never checked) prefetches read the
     // pair's own boundary area, which is always inside the workspace
@@ -712,9 +718,9 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
         // this lane's columns for steps s0..s0+7: E[s0 - lane], E[s0 - lane + 4]
         const unsigned e0 = ewin[blk * 8 + 64 - lane], e1 = ewin[blk * 8 + 68 - lane];
         if (sb == 0)
-          step_block<MODE, W, true>(s0, lane, h, Up, stage, acc, xq, e0, e1, slot + blk * 8, mptr, a.K0, a.K1);
+          step_block<MODE, W, true>(s0, lane, h, Up, stage, acc, xq, e0, e1, slot + blk * 8, mptr, a.K0, a.K1, store);
         else
-          step_block<MODE, W, false>(s0, lane, h, Up, stage, acc, xq, e0, e1, slot + blk * 8, mptr, a.K0, a.K1);
+          step_block<MODE, W, false>(s0, lane, h, Up, stage, acc, xq, e0, e1, slot + blk * 8, mptr, a.K0, a.K1, store);
         mptr += (8 / SPD) * kRows * kWave;
         // the window / granule prefetches are older than this block's
         // kBlockStores stores: waiting for the rest leaves those in flight
@@ -738,16 +744,27 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
       atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 1, (unsigned long long)n_wait);
       atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 2, (unsigned long long)pd.sblocks);
     }
+    if (a.lin_mode == 1) continue;  // fill pass of the linear-space traceback: no trace
     unsigned prev = 0;
     if (lane == 0) prev = __hip_atomic_fetch_add((gu32*)(a.done + pd.slot), 1u, RLX_AGENT);
     prev = __builtin_amdgcn_readfirstlane(prev);
     // --- the pair's last band: every band wave has released, so acquire and
     // trace the pair here while the other waves keep filling.
-    if (prev + 1u == (unsigned)pd.nbands) {
+    if (prev + 1u == (unsigned)(a.lin_mode == 2 ? pd.lin_nb : pd.nbands)) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
-      trace_whole<W>(a, pd, tbl[wid], lane);
+      if (a.lin_mode == 2) {  // one group: from (lin_i, lin_j) up to the group's top row
+        SegCtx sc{a.ops + pd.ops_off, pd.lin_i, pd.lin_j, 0, nullptr, nullptr, 0, nullptr};
+        sc.stop = pd.lin_stop;
+        const SegOut o = trace_pair<W>(a, pd, tbl[wid], lane, sc);
+        if (lane == 0) {
+          a.oplen[pd.slot] = o.len;
+          a.endij[pd.slot] = make_int2(o.ei, o.ej);
+        }
+      } else {
+        trace_whole<W>(a, pd, tbl[wid], lane);
+      }
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
     }
   }

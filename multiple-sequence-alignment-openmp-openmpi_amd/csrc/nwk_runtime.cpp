@@ -525,6 +525,143 @@ struct Chain {
   }
 };
 
+// Linear-space traceback of one pair whose DP matrix does not
+// fit the HBM budget (or of every pair when opts.linear_space = G > 0).
+// Pass 1 fills all bands keeping only their boundary rows (the granules,
+// m/512 x n x 8 B).  Then, from the bottom up, a group of G bands plus the
+// band above it (whose last row the trace reads) is recomputed -- all bands of
+// the group at once, each from the stored boundary row above it -- into a
+// scratch matrix of G + 1 bands, and the trace walks through the group to its
+// top row.  Same kernel (nw_align, plain layout) and tie-breaks as the stored
+// path, so the results are identical; the price is a second fill.
+int align_linear_pair(nwk_ctx* c, const Plan& pl0, const Scoring& sc, const PairWork& w, int G, Finalized* out,
+                      std::vector<uint8_t>* a1, std::vector<uint8_t>* a2, nwk_stats* st) {
+  Plan pl = pl0;
+  if (pl.mode == kPacked || pl.mode == kPacked2) pl.mode = kProfile;  // same bits (4), codes and K0/K1
+  int rc;
+  const int nb = (int)ceil_div(w.m, kBandRows);
+  const int nch = (int)ceil_div(w.n, 64);
+  const int sbl = sblocks_of(pl.mode, nch);
+  const int64_t bdw = band_dwords(pl.bits, sbl);
+  const int64_t bnd_need_b = (int64_t)std::max(1, nb - 1) * nch * 64 * 8 + 4096;
+  const int64_t scratch_b0 = round_up(bnd_need_b, 256);
+  if (G <= 0) {  // as many bands per group as the budget holds
+    const int64_t avail = c->budget - scratch_b0 - 2 * ((int64_t)w.m + w.n) - (1ll << 20);
+    G = (int)std::min<int64_t>(nb, avail / (bdw * 4) - 1);
+    if (G < 1)
+      return fail(NWK_ENOMEM, "pair (%d x %d): boundary rows and two bands (%lld bytes) exceed the HBM budget %lld",
+                  w.m, w.n, (long long)(scratch_b0 + 2 * bdw * 4), (long long)c->budget);
+  }
+  G = std::min(G, nb);
+  const int ngroups = (int)ceil_div(nb, G);
+  const int64_t ops_base_b = scratch_b0 + round_up((int64_t)(G + 1) * bdw * 4, 256);
+  const int64_t ops_cap = round_up((int64_t)w.m + w.n + 16 * (ngroups + 1), 16);
+  const int64_t work_b = ops_base_b + ops_cap + 4096;
+  void* const old_work = c->d_work.p;
+  if ((rc = c->d_work.ensure((size_t)work_b)) != NWK_OK) return rc;
+  if (c->d_work.p != old_work) c->clean_b = 0;
+  if (bnd_need_b > c->clean_b)
+    HIP_TRY(hipMemsetAsync(c->d_work.as<uint8_t>() + c->clean_b, 0, (size_t)(bnd_need_b - c->clean_b), c->stream));
+  c->clean_b = bnd_need_b;
+  if ((rc = c->d_pairs.ensure(sizeof(PairDesc))) != NWK_OK) return rc;
+  if ((rc = c->d_tasks.ensure(sizeof(int2) * nb)) != NWK_OK) return rc;
+  if ((rc = c->d_oplen.ensure(sizeof(int))) != NWK_OK) return rc;
+  if ((rc = c->d_endij.ensure(sizeof(int2))) != NWK_OK) return rc;
+  if ((rc = c->d_done.ensure(sizeof(unsigned))) != NWK_OK) return rc;
+  PairDesc d;
+  memset(&d, 0, sizeof d);
+  d.x_off = c->c_off[w.i];
+  d.y_off = c->c_off[w.j];
+  d.e_off = c->e_off[w.j];
+  d.mat_off = scratch_b0 / 4;
+  d.m = w.m;
+  d.n = w.n;
+  d.nbands = nb;
+  d.nchunks = nch;
+  d.sblocks = sbl;
+  FillArgs fa;
+  memset(&fa, 0, sizeof fa);
+  fa.pairs = c->d_pairs.as<PairDesc>();
+  fa.tasks = c->d_tasks.as<int2>();
+  fa.codes = c->d_codes[pl.kind].as<uint8_t>();
+  fa.E = c->d_E[pl.kind].as<uint32_t>();
+  fa.mat = c->d_work.as<uint32_t>();
+  fa.bnd = c->d_work.as<unsigned long long>();
+  fa.counter = c->d_ctl.as<unsigned>();
+  fa.err = c->d_ctl.as<unsigned>() + 16;
+  fa.done = c->d_done.as<unsigned>();
+  fa.ops = c->d_work.as<uint8_t>();
+  fa.oplen = c->d_oplen.as<int>();
+  fa.endij = c->d_endij.as<int2>();
+  fa.epoch = ++c->epoch;  // pass 2 reads pass 1's boundary rows under the same epoch
+  if (fa.epoch == 0) fa.epoch = ++c->epoch;
+  fa.K0 = pl.K0;
+  fa.K1 = pl.K1;
+  fa.ntasks_pairs = 1;
+  const int grid = fill_blocks_per_cu(pl.mode, pl.bits) * c->cus;
+  std::vector<int2> tk((size_t)nb);
+  int ol = 0;
+  int2 ej = make_int2(w.m, w.n);
+  // one launch over bands [b0, b1] of the pair, waited for
+  auto launch = [&](int mode, int b0, int b1, double* ms_acc) -> int {
+    const int nt = b1 - b0 + 1;
+    for (int b = b0; b <= b1; ++b) tk[b - b0] = make_int2(0, b);
+    HIP_TRY(hipMemcpyAsync(c->d_pairs.p, &d, sizeof d, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_tasks.p, tk.data(), sizeof(int2) * nt, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_ctl.p, 0, 256, c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_done.p, 0, sizeof(unsigned), c->stream));
+    fa.ntasks = nt;
+    fa.lin_mode = mode;
+    HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+    HIP_TRY(launch_fill(pl.mode, pl.bits, fa, (int)std::min<int64_t>(grid, ceil_div(nt, 4)), c->stream));
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    unsigned herr = 0;
+    HIP_TRY(hipMemcpyAsync(&herr, fa.err, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&ol, fa.oplen, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&ej, fa.endij, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (herr) return fail(NWK_EKERNEL, "linear-space pass %d of pair (%d x %d) failed (err=%u)", mode, w.m, w.n, herr);
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    *ms_acc += ms;
+    st->fill_launches += 1;
+    return NWK_OK;
+  };
+  if ((rc = launch(1, 0, nb - 1, &st->fill_ms)) != NWK_OK) return rc;
+  int i = w.m, j = w.n;
+  int64_t off = 0;
+  std::vector<std::pair<int64_t, int>> pieces;
+  while (i > 0 && j > 0) {
+    const int gb1 = (i - 1) / kBandRows;
+    const int b0 = std::max(0, gb1 - G + 1);
+    const int gb0 = std::max(0, b0 - 1);
+    d.mat_off = scratch_b0 / 4 - (int64_t)gb0 * bdw;  // band b of the group at scratch + (b - gb0) bands
+    d.ops_off = ops_base_b + off;
+    d.lin_nb = gb1 - gb0 + 1;
+    d.lin_i = i;
+    d.lin_j = j;
+    d.lin_stop = b0 * kBandRows;
+    if ((rc = launch(2, gb0, gb1, &st->traceback_ms)) != NWK_OK) return rc;
+    if (ol < 0 || off + ol > ops_cap || ej.x > i || ej.y > j || (ej.x == i && ej.y == j))
+      return fail(NWK_EKERNEL, "linear-space trace of pair (%d x %d) stalled at (%d, %d)", w.m, w.n, i, j);
+    pieces.emplace_back(off, ol);
+    off += round_up(ol, 16);
+    i = ej.x;
+    j = ej.y;
+  }
+  std::vector<uint8_t> buf((size_t)std::max<int64_t>(off, 1)), rev;
+  if (off > 0)
+    HIP_TRY(hipMemcpy(buf.data(), c->d_work.as<uint8_t>() + ops_base_b, (size_t)off, hipMemcpyDeviceToHost));
+  rev.reserve((size_t)w.m + w.n);
+  for (const auto& pc : pieces) rev.insert(rev.end(), buf.begin() + pc.first, buf.begin() + pc.first + pc.second);
+  finalize_pair(c->seqs.data() + c->off[w.i], w.m, c->seqs.data() + c->off[w.j], w.n, sc, rev.data(), (int)rev.size(),
+                i, j, out, a1, a2);
+  st->matrix_bytes += (int64_t)(G + 1) * bdw * 4;
+  st->linear_space_pairs += 1;
+  st->batches += 1;
+  return NWK_OK;
+}
+
 int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32_t* penalties,
                uint8_t* hashes, std::vector<uint8_t>* a1, std::vector<uint8_t>* a2, Chain* chain = nullptr) {
   const double t_start = now_ms();
@@ -640,19 +777,39 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   if (dev_ok && !dp.empty() && (rc = build_encoding(c, 1)) != NWK_OK) return rc;
   size_t pos = 0;
   double h_setup = 0, h_sync = 0, h_join = 0, h_last = 0;  // host phases (verbose)
+  const bool lin_all = c->opts.linear_space > 0 && !sc.affine;  // (tests: every pair through f2)
   while (pos < dp.size()) {
     // ---- form a batch that fits the HBM budget
     size_t end = pos;
+    bool lin_one = false;
     int64_t mat = 0, bnd = 0, ops = 0, segops = 0;
     while (end < dp.size()) {
       const PairWork& w = dp[end];
       const int64_t need = (mat + w.mat_dw) * 4 + (bnd + w.bnd_gr) * 8 + 3 * (ops + w.ops_b) + segops + w.segops_b + 8192;
-      if (need > c->budget && end > pos) break;
-      if (need > c->budget)
-        return fail(NWK_ENOMEM, "pair %lld (%d x %d) needs %lld bytes > HBM budget %lld", (long long)w.id,
-                    w.m, w.n, (long long)need, (long long)c->budget);
+      if ((need > c->budget || lin_all) && end > pos) break;
+      if (need > c->budget || lin_all) {  // a pair whose matrix does not fit: linear-space traceback (f2)
+        if (c->opts.linear_space < 0 || sc.affine)
+          return fail(NWK_ENOMEM, "pair %lld (%d x %d) needs %lld bytes > HBM budget %lld", (long long)w.id,
+                      w.m, w.n, (long long)need, (long long)c->budget);
+        lin_one = true;
+        break;
+      }
       mat += w.mat_dw; bnd += w.bnd_gr; ops += w.ops_b; segops += w.segops_b;
       ++end;
+    }
+    if (lin_one) {
+      fin.join();
+      const PairWork& w = dp[pos];
+      Finalized f;
+      if ((rc = align_linear_pair(c, pl, sc, w, std::max(0, c->opts.linear_space), &f, a1, a2, &st)) != NWK_OK) return rc;
+      penalties[w.out] = f.penalty;
+      memcpy(hashes + 64 * w.out, f.hash, 64);
+      if (chain) {
+        chain->ready[w.out] = 1;
+        chain->advance();
+      }
+      ++pos;
+      continue;
     }
     const int np = (int)(end - pos);
     const double tb0 = now_ms();
@@ -791,6 +948,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.K1 = pl.K1;
     fa.go = sc.go;
     fa.dbg_notrace = (getenv("NWK_AFF_NOTRACE") || getenv("NWK_NOTRACE")) ? 1 : 0;
+    fa.lin_mode = 0;
     fa.prog = nullptr;
     if (getenv("NWK_WATCHDOG")) {
       if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;

@@ -35,7 +35,8 @@ class NwkError(RuntimeError):
 class Opts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("ngpus", ctypes.c_int32), ("bits", ctypes.c_int32),
                 ("host_threads", ctypes.c_int32), ("workspace_bytes", ctypes.c_int64),
-                ("verbose", ctypes.c_int32), ("finalize", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
+                ("verbose", ctypes.c_int32), ("finalize", ctypes.c_int32),
+                ("linear_space", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
 
 
 class Stats(ctypes.Structure):
@@ -44,7 +45,7 @@ class Stats(ctypes.Structure):
                 ("matrix_bytes", ctypes.c_int64), ("batches", ctypes.c_int32),
                 ("bits", ctypes.c_int32), ("mode", ctypes.c_int32),
                 ("fill_launches", ctypes.c_int32), ("device_finalized", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 3)]
+                ("linear_space_pairs", ctypes.c_int32), ("reserved", ctypes.c_int32 * 2)]
 
 
 # Every exported symbol of include/nwk.h with its ctypes signature.
@@ -141,7 +142,8 @@ class Engine:
 
     FINALIZE = {"auto": 0, "host": 1, "device": 2}
 
-    def __init__(self, device=0, bits=0, workspace_bytes=0, host_threads=0, verbose=False, finalize="auto"):
+    def __init__(self, device=0, bits=0, workspace_bytes=0, host_threads=0, verbose=False, finalize="auto",
+                 linear_space=0):
         """finalize: where rows, penalty and SHA-512 of each pair are computed --
         "auto" (per batch, by estimated cost), "host" threads, or "device" (nw_hash)."""
         self.lib = load_library()
@@ -150,6 +152,9 @@ class Engine:
         o.device, o.bits, o.workspace_bytes = device, bits, workspace_bytes
         o.host_threads, o.verbose = host_threads, int(verbose)
         o.finalize = self.FINALIZE[finalize]
+        # linear-space traceback: 0 only where the matrix does not fit,
+        # -1 never, G > 0 every pair with G bands per recompute group
+        o.linear_space = linear_space
         self._ctx = ctypes.c_void_p()
         _check(self.lib.nwk_ctx_create(ctypes.byref(o), ctypes.byref(self._ctx)))
         self.k = 0

@@ -399,3 +399,66 @@ def test_msa_rejects_what_it_cannot_align(engine):
     engine.set_sequences([b"ABCDEF", b"AB"])
     with pytest.raises(seqalign.NwkError):
         engine.msa(3, 2)
+
+
+# --- linear-space traceback: boundary rows only, bands recomputed per group
+
+SMALL_GOLDEN = [c for c in GOLDEN if sum(len(g) for g in case_input(c)[2]) < 100000]
+
+
+@pytest.mark.parametrize("g", [1, 3])
+@pytest.mark.parametrize("case", SMALL_GOLDEN, ids=[c["name"] for c in SMALL_GOLDEN])
+def test_linear_space_golden(g, case):
+    pxy, pgap, genes = case_input(case)
+    with seqalign.Engine(device=0, linear_space=g) as e:
+        e.set_sequences(genes)
+        pen, hs = e.align_pairs(_all_ids(len(genes)), pxy, pgap)
+        st = e.stats()
+    assert [int(v) for v in pen] == case["penalties"]
+    assert seqalign.chain_hash(hs) == case["hash"]
+    assert st["linear_space_pairs"] == sum(1 for i in range(len(genes)) for j in range(i)
+                                           if len(genes[i]) and len(genes[j]))
+
+
+@pytest.mark.parametrize("g", [1, 2, 5])
+def test_linear_space_random_vs_oracle(g):
+    r = random.Random(900 + g)
+    genes = _rand_genes(r, 3, 1, 3000, ACGT) + _mutants(r, _rand_genes(r, 1, 2500, 2600, ACGT)[0], 2, ACGT)
+    with seqalign.Engine(device=0, linear_space=g) as e:
+        e.set_sequences(genes)
+        for pxy, pgap in ((3, 2), (5, 1), (1, 0), (40000, 30000)):
+            pen, hs = e.align_pairs(_all_ids(len(genes)), pxy, pgap)
+            h, want, _ = oracle.all_pairs(genes, pxy, pgap)
+            assert [int(v) for v in pen] == want, (pxy, pgap)
+            assert seqalign.chain_hash(hs) == h, (pxy, pgap)
+
+
+def test_linear_space_single_pair_rows():
+    r = random.Random(77)
+    x, y = (bytes(r.choice(ACGT) for _ in range(n)) for n in (2600, 1900))
+    with seqalign.Engine(device=0, linear_space=2) as e:
+        assert e.get_minimum_penalty(x, y, 3, 2) == oracle.pair(x, y, 3, 2)
+
+
+def test_linear_space_when_the_matrix_does_not_fit():
+    """Automatic: a pair whose stored matrix exceeds the HBM budget goes through f2."""
+    r = random.Random(5)
+    genes = [bytes(r.choice(ACGT) for _ in range(6000)) for _ in range(2)] + [b"ACGT" * 10]
+    with seqalign.Engine(device=0, workspace_bytes=8 << 20) as e:
+        e.set_sequences(genes)
+        pen, hs = e.align_pairs(_all_ids(3), 3, 2)
+        st = e.stats()
+    h, want, _ = oracle.all_pairs(genes, 3, 2)
+    assert [int(v) for v in pen] == want and seqalign.chain_hash(hs) == h
+    assert st["linear_space_pairs"] >= 1
+
+
+def test_linear_space_big13(golden):
+    """Full size (2.785e11 cells) through the linear-space path: the reference's published hash."""
+    c = golden["big13"]
+    pxy, pgap, genes = case_input(c)
+    with seqalign.Engine(device=0, linear_space=16) as e:
+        e.set_sequences(genes)
+        pen, hs = e.align_pairs(_all_ids(len(genes)), pxy, pgap)
+    assert [int(v) for v in pen] == c["penalties"]
+    assert seqalign.chain_hash(hs) == c["hash"]
