@@ -525,60 +525,97 @@ struct Chain {
   }
 };
 
-// Linear-space traceback of one pair whose DP matrix does not
-// fit the HBM budget (or of every pair when opts.linear_space = G > 0).
+// Linear-space traceback for pairs whose DP matrix does not
+// fit the HBM budget (or for every pair when opts.linear_space = G > 0).
 // Pass 1 fills all bands keeping only their boundary rows (the granules,
 // m/512 x n x 8 B).  Then, from the bottom up, a group of G bands plus the
 // band above it (whose last row the trace reads) is recomputed -- all bands of
 // the group at once, each from the stored boundary row above it -- into a
 // scratch matrix of G + 1 bands, and the trace walks through the group to its
 // top row.  Same kernel (nw_align, plain layout) and tie-breaks as the stored
-// path, so the results are identical; the price is a second fill.
-int align_linear_pair(nwk_ctx* c, const Plan& pl0, const Scoring& sc, const PairWork& w, int G, Finalized* out,
-                      std::vector<uint8_t>* a1, std::vector<uint8_t>* a2, nwk_stats* st) {
+// path, so the results are identical; the price is a second fill.  The pairs
+// of a batch share every launch: pass 1 is one launch, and each round
+// recomputes and traces the current group of every pair still tracing.
+struct LinGeo {
+  int nb, nch, sbl, G, ngroups;
+  int64_t bdw, bnd_gr, scratch_dw, ops_cap, bytes;
+};
+
+LinGeo lin_geo(const Plan& pl, const PairWork& w, int G) {
+  LinGeo g;
+  g.nb = (int)ceil_div(w.m, kBandRows);
+  g.nch = (int)ceil_div(w.n, 64);
+  g.sbl = sblocks_of(pl.mode, g.nch);
+  g.bdw = band_dwords(pl.bits, g.sbl);
+  g.G = std::max(1, std::min(G, g.nb));
+  g.ngroups = (int)ceil_div(g.nb, g.G);
+  g.bnd_gr = (int64_t)std::max(1, g.nb - 1) * g.nch * 64;
+  g.scratch_dw = (int64_t)(g.G + 1) * g.bdw;
+  g.ops_cap = round_up((int64_t)w.m + w.n + 16 * (g.ngroups + 1), 16);
+  g.bytes = g.bnd_gr * 8 + g.scratch_dw * 4 + g.ops_cap + 1024;
+  return g;
+}
+
+Plan lin_plan(const Plan& pl0) {
   Plan pl = pl0;
   if (pl.mode == kPacked || pl.mode == kPacked2) pl.mode = kProfile;  // same bits (4), codes and K0/K1
+  return pl;
+}
+
+// G for one pair alone in the budget (0 if even two bands do not fit)
+int lin_auto_groups(const nwk_ctx* c, const Plan& pl, const PairWork& w) {
+  const LinGeo g = lin_geo(pl, w, 1);
+  const int64_t avail = c->budget - g.bnd_gr * 8 - 2 * ((int64_t)w.m + w.n) - (1ll << 20);
+  const int64_t G = avail / (g.bdw * 4) - 1;
+  return G < 1 ? 0 : (int)std::min<int64_t>(G, g.nb);
+}
+
+int align_linear_batch(nwk_ctx* c, const Plan& pl0, const Scoring& sc, const PairWork* ws, int np, int G,
+                       Finalized* outs, std::vector<uint8_t>* a1, std::vector<uint8_t>* a2, nwk_stats* st) {
+  const Plan pl = lin_plan(pl0);
   int rc;
-  const int nb = (int)ceil_div(w.m, kBandRows);
-  const int nch = (int)ceil_div(w.n, 64);
-  const int sbl = sblocks_of(pl.mode, nch);
-  const int64_t bdw = band_dwords(pl.bits, sbl);
-  const int64_t bnd_need_b = (int64_t)std::max(1, nb - 1) * nch * 64 * 8 + 4096;
-  const int64_t scratch_b0 = round_up(bnd_need_b, 256);
-  if (G <= 0) {  // as many bands per group as the budget holds
-    const int64_t avail = c->budget - scratch_b0 - 2 * ((int64_t)w.m + w.n) - (1ll << 20);
-    G = (int)std::min<int64_t>(nb, avail / (bdw * 4) - 1);
-    if (G < 1)
-      return fail(NWK_ENOMEM, "pair (%d x %d): boundary rows and two bands (%lld bytes) exceed the HBM budget %lld",
-                  w.m, w.n, (long long)(scratch_b0 + 2 * bdw * 4), (long long)c->budget);
+  std::vector<LinGeo> geo((size_t)np);
+  std::vector<PairDesc> pd((size_t)np);
+  std::vector<int64_t> scr_off((size_t)np), ops_off((size_t)np);
+  int64_t bnd = 0, scr = 0, ops = 0, ntasks = 0;
+  for (int q = 0; q < np; ++q) {
+    const PairWork& w = ws[q];
+    const LinGeo& g = geo[q] = lin_geo(pl, w, G);
+    PairDesc& d = pd[q];
+    memset(&d, 0, sizeof d);
+    d.x_off = c->c_off[w.i];
+    d.y_off = c->c_off[w.j];
+    d.e_off = c->e_off[w.j];
+    d.bnd_off = bnd;
+    d.m = w.m;
+    d.n = w.n;
+    d.nbands = g.nb;
+    d.nchunks = g.nch;
+    d.sblocks = g.sbl;
+    d.slot = q;
+    scr_off[q] = scr;
+    ops_off[q] = ops;
+    bnd += g.bnd_gr;
+    scr += g.scratch_dw;
+    ops += g.ops_cap;
+    ntasks += g.nb;
   }
-  G = std::min(G, nb);
-  const int ngroups = (int)ceil_div(nb, G);
-  const int64_t ops_base_b = scratch_b0 + round_up((int64_t)(G + 1) * bdw * 4, 256);
-  const int64_t ops_cap = round_up((int64_t)w.m + w.n + 16 * (ngroups + 1), 16);
-  const int64_t work_b = ops_base_b + ops_cap + 4096;
+  const int64_t bnd_need_b = bnd * 8 + 4096;
+  const int64_t scratch_b0 = round_up(bnd_need_b, 256);
+  const int64_t ops_base_b = scratch_b0 + round_up(scr * 4, 256);
+  const int64_t work_b = ops_base_b + ops + 4096;
   void* const old_work = c->d_work.p;
   if ((rc = c->d_work.ensure((size_t)work_b)) != NWK_OK) return rc;
   if (c->d_work.p != old_work) c->clean_b = 0;
   if (bnd_need_b > c->clean_b)
     HIP_TRY(hipMemsetAsync(c->d_work.as<uint8_t>() + c->clean_b, 0, (size_t)(bnd_need_b - c->clean_b), c->stream));
   c->clean_b = bnd_need_b;
-  if ((rc = c->d_pairs.ensure(sizeof(PairDesc))) != NWK_OK) return rc;
-  if ((rc = c->d_tasks.ensure(sizeof(int2) * nb)) != NWK_OK) return rc;
-  if ((rc = c->d_oplen.ensure(sizeof(int))) != NWK_OK) return rc;
-  if ((rc = c->d_endij.ensure(sizeof(int2))) != NWK_OK) return rc;
-  if ((rc = c->d_done.ensure(sizeof(unsigned))) != NWK_OK) return rc;
-  PairDesc d;
-  memset(&d, 0, sizeof d);
-  d.x_off = c->c_off[w.i];
-  d.y_off = c->c_off[w.j];
-  d.e_off = c->e_off[w.j];
-  d.mat_off = scratch_b0 / 4;
-  d.m = w.m;
-  d.n = w.n;
-  d.nbands = nb;
-  d.nchunks = nch;
-  d.sblocks = sbl;
+  if ((rc = c->d_pairs.ensure(sizeof(PairDesc) * np)) != NWK_OK) return rc;
+  if ((rc = c->d_tasks.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
+  if ((rc = c->d_oplen.ensure(sizeof(int) * np)) != NWK_OK) return rc;
+  if ((rc = c->d_endij.ensure(sizeof(int2) * np)) != NWK_OK) return rc;
+  if ((rc = c->d_done.ensure(sizeof(unsigned) * np)) != NWK_OK) return rc;
+  for (int q = 0; q < np; ++q) pd[q].mat_off = scratch_b0 / 4 + scr_off[q];
   FillArgs fa;
   memset(&fa, 0, sizeof fa);
   fa.pairs = c->d_pairs.as<PairDesc>();
@@ -593,71 +630,90 @@ int align_linear_pair(nwk_ctx* c, const Plan& pl0, const Scoring& sc, const Pair
   fa.ops = c->d_work.as<uint8_t>();
   fa.oplen = c->d_oplen.as<int>();
   fa.endij = c->d_endij.as<int2>();
-  fa.epoch = ++c->epoch;  // pass 2 reads pass 1's boundary rows under the same epoch
+  fa.epoch = ++c->epoch;  // the group passes read pass 1's boundary rows under the same epoch
   if (fa.epoch == 0) fa.epoch = ++c->epoch;
   fa.K0 = pl.K0;
   fa.K1 = pl.K1;
-  fa.ntasks_pairs = 1;
+  fa.ntasks_pairs = np;
   const int grid = fill_blocks_per_cu(pl.mode, pl.bits) * c->cus;
-  std::vector<int2> tk((size_t)nb);
-  int ol = 0;
-  int2 ej = make_int2(w.m, w.n);
-  // one launch over bands [b0, b1] of the pair, waited for
-  auto launch = [&](int mode, int b0, int b1, double* ms_acc) -> int {
-    const int nt = b1 - b0 + 1;
-    for (int b = b0; b <= b1; ++b) tk[b - b0] = make_int2(0, b);
-    HIP_TRY(hipMemcpyAsync(c->d_pairs.p, &d, sizeof d, hipMemcpyHostToDevice, c->stream));
+  std::vector<int2> tk;
+  tk.reserve((size_t)ntasks);
+  std::vector<int> ol((size_t)np, 0);
+  std::vector<int2> ej((size_t)np);
+  // one launch over the tasks in tk, waited for
+  auto launch = [&](int mode, double* ms_acc) -> int {
+    const int64_t nt = (int64_t)tk.size();
+    HIP_TRY(hipMemcpyAsync(c->d_pairs.p, pd.data(), sizeof(PairDesc) * np, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_tasks.p, tk.data(), sizeof(int2) * nt, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(c->d_ctl.p, 0, 256, c->stream));
-    HIP_TRY(hipMemsetAsync(c->d_done.p, 0, sizeof(unsigned), c->stream));
-    fa.ntasks = nt;
+    HIP_TRY(hipMemsetAsync(c->d_done.p, 0, sizeof(unsigned) * np, c->stream));
+    fa.ntasks = (int)nt;
     fa.lin_mode = mode;
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(launch_fill(pl.mode, pl.bits, fa, (int)std::min<int64_t>(grid, ceil_div(nt, 4)), c->stream));
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     unsigned herr = 0;
     HIP_TRY(hipMemcpyAsync(&herr, fa.err, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(&ol, fa.oplen, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(&ej, fa.endij, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(ol.data(), fa.oplen, 4 * (size_t)np, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(ej.data(), fa.endij, 8 * (size_t)np, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (herr) return fail(NWK_EKERNEL, "linear-space pass %d of pair (%d x %d) failed (err=%u)", mode, w.m, w.n, herr);
+    if (herr) return fail(NWK_EKERNEL, "linear-space pass %d of a %d-pair batch failed (err=%u)", mode, np, herr);
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     *ms_acc += ms;
     st->fill_launches += 1;
     return NWK_OK;
   };
-  if ((rc = launch(1, 0, nb - 1, &st->fill_ms)) != NWK_OK) return rc;
-  int i = w.m, j = w.n;
-  int64_t off = 0;
-  std::vector<std::pair<int64_t, int>> pieces;
-  while (i > 0 && j > 0) {
-    const int gb1 = (i - 1) / kBandRows;
-    const int b0 = std::max(0, gb1 - G + 1);
-    const int gb0 = std::max(0, b0 - 1);
-    d.mat_off = scratch_b0 / 4 - (int64_t)gb0 * bdw;  // band b of the group at scratch + (b - gb0) bands
-    d.ops_off = ops_base_b + off;
-    d.lin_nb = gb1 - gb0 + 1;
-    d.lin_i = i;
-    d.lin_j = j;
-    d.lin_stop = b0 * kBandRows;
-    if ((rc = launch(2, gb0, gb1, &st->traceback_ms)) != NWK_OK) return rc;
-    if (ol < 0 || off + ol > ops_cap || ej.x > i || ej.y > j || (ej.x == i && ej.y == j))
-      return fail(NWK_EKERNEL, "linear-space trace of pair (%d x %d) stalled at (%d, %d)", w.m, w.n, i, j);
-    pieces.emplace_back(off, ol);
-    off += round_up(ol, 16);
-    i = ej.x;
-    j = ej.y;
+  for (int q = 0; q < np; ++q)
+    for (int b = 0; b < geo[q].nb; ++b) tk.push_back(make_int2(q, b));
+  if ((rc = launch(1, &st->fill_ms)) != NWK_OK) return rc;
+  std::vector<int> ci((size_t)np), cj((size_t)np);
+  std::vector<int64_t> off((size_t)np, 0);
+  std::vector<std::vector<std::pair<int64_t, int>>> pieces((size_t)np);
+  for (int q = 0; q < np; ++q) ci[q] = ws[q].m, cj[q] = ws[q].n;
+  for (;;) {
+    tk.clear();
+    std::vector<int> act;
+    for (int q = 0; q < np; ++q) {
+      if (ci[q] <= 0 || cj[q] <= 0) continue;
+      const LinGeo& g = geo[q];
+      const int gb1 = (ci[q] - 1) / kBandRows;
+      const int b0 = std::max(0, gb1 - g.G + 1);
+      const int gb0 = std::max(0, b0 - 1);
+      PairDesc& d = pd[q];
+      d.mat_off = scratch_b0 / 4 + scr_off[q] - (int64_t)gb0 * g.bdw;  // band b at scratch + (b - gb0) bands
+      d.ops_off = ops_base_b + ops_off[q] + off[q];
+      d.lin_nb = gb1 - gb0 + 1;
+      d.lin_i = ci[q];
+      d.lin_j = cj[q];
+      d.lin_stop = b0 * kBandRows;
+      for (int b = gb0; b <= gb1; ++b) tk.push_back(make_int2(q, b));
+      act.push_back(q);
+    }
+    if (act.empty()) break;
+    if ((rc = launch(2, &st->traceback_ms)) != NWK_OK) return rc;
+    for (int q : act) {
+      if (ol[q] < 0 || off[q] + ol[q] > geo[q].ops_cap || ej[q].x > ci[q] || ej[q].y > cj[q] ||
+          (ej[q].x == ci[q] && ej[q].y == cj[q]))
+        return fail(NWK_EKERNEL, "linear-space trace of pair (%d x %d) stalled at (%d, %d)", ws[q].m, ws[q].n, ci[q], cj[q]);
+      pieces[q].emplace_back(off[q], ol[q]);
+      off[q] += round_up(ol[q], 16);
+      ci[q] = ej[q].x;
+      cj[q] = ej[q].y;
+    }
   }
-  std::vector<uint8_t> buf((size_t)std::max<int64_t>(off, 1)), rev;
-  if (off > 0)
-    HIP_TRY(hipMemcpy(buf.data(), c->d_work.as<uint8_t>() + ops_base_b, (size_t)off, hipMemcpyDeviceToHost));
-  rev.reserve((size_t)w.m + w.n);
-  for (const auto& pc : pieces) rev.insert(rev.end(), buf.begin() + pc.first, buf.begin() + pc.first + pc.second);
-  finalize_pair(c->seqs.data() + c->off[w.i], w.m, c->seqs.data() + c->off[w.j], w.n, sc, rev.data(), (int)rev.size(),
-                i, j, out, a1, a2);
-  st->matrix_bytes += (int64_t)(G + 1) * bdw * 4;
-  st->linear_space_pairs += 1;
+  std::vector<uint8_t> buf((size_t)std::max<int64_t>(ops, 1));
+  HIP_TRY(hipMemcpy(buf.data(), c->d_work.as<uint8_t>() + ops_base_b, (size_t)ops, hipMemcpyDeviceToHost));
+  parallel_for(a1 ? 1 : c->host_threads, np, [&](int64_t q) {
+    std::vector<uint8_t> rev;
+    rev.reserve((size_t)ws[q].m + ws[q].n);
+    const uint8_t* base = buf.data() + ops_off[q];
+    for (const auto& pc : pieces[q]) rev.insert(rev.end(), base + pc.first, base + pc.first + pc.second);
+    finalize_pair(c->seqs.data() + c->off[ws[q].i], ws[q].m, c->seqs.data() + c->off[ws[q].j], ws[q].n, sc, rev.data(),
+                  (int)rev.size(), ci[q], cj[q], &outs[q], a1, a2);
+  });
+  for (int q = 0; q < np; ++q) st->matrix_bytes += geo[q].scratch_dw * 4;
+  st->linear_space_pairs += np;
   st->batches += 1;
   return NWK_OK;
 }
@@ -799,16 +855,32 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     }
     if (lin_one) {
       fin.join();
-      const PairWork& w = dp[pos];
-      Finalized f;
-      if ((rc = align_linear_pair(c, pl, sc, w, std::max(0, c->opts.linear_space), &f, a1, a2, &st)) != NWK_OK) return rc;
-      penalties[w.out] = f.penalty;
-      memcpy(hashes + 64 * w.out, f.hash, 64);
-      if (chain) {
-        chain->ready[w.out] = 1;
-        chain->advance();
+      // forced (tests): as many pairs per linear-space batch as fit; automatic:
+      // the pair that does not fit, alone, with as many bands per group as fit
+      const Plan lpl = lin_plan(pl);
+      const int G = lin_all ? c->opts.linear_space : lin_auto_groups(c, lpl, dp[pos]);
+      if (G < 1)
+        return fail(NWK_ENOMEM, "pair (%d x %d): boundary rows and two bands exceed the HBM budget %lld", dp[pos].m,
+                    dp[pos].n, (long long)c->budget);
+      size_t lend = pos + 1;
+      int64_t used = lin_geo(lpl, dp[pos], G).bytes;
+      while (lin_all && lend < dp.size()) {
+        const int64_t more = lin_geo(lpl, dp[lend], G).bytes;
+        if (used + more + 8192 > c->budget) break;
+        used += more;
+        ++lend;
       }
-      ++pos;
+      const int nl = (int)(lend - pos);
+      std::vector<Finalized> fs((size_t)nl);
+      if ((rc = align_linear_batch(c, pl, sc, dp.data() + pos, nl, G, fs.data(), a1, a2, &st)) != NWK_OK) return rc;
+      for (int q = 0; q < nl; ++q) {
+        const PairWork& w = dp[pos + q];
+        penalties[w.out] = fs[q].penalty;
+        memcpy(hashes + 64 * w.out, fs[q].hash, 64);
+        if (chain) chain->ready[w.out] = 1;
+      }
+      if (chain) chain->advance();
+      pos = lend;
       continue;
     }
     const int np = (int)(end - pos);
