@@ -11,6 +11,9 @@
 //                                   whitespace removed)
 //   --dump FILE                     per pair in canonical order: "i j penalty",
 //                                   then align1 and align2 (trimmed rows) lines
+//   --msa FILE                      progressive sum-of-pairs MSA (SURVEY §8 f3,
+//                                   nwk_msa) as FASTA: ">seq<i> sop=<score>"
+//                                   headers, one aligned row per record
 //
 // The timed span is the getMinimumPenalties call (skel:53-61), here
 // nwk_get_minimum_penalties.  No MPI: the reference's ranks become devices
@@ -78,13 +81,33 @@ static int dump_pairs(const char* path, const std::vector<std::string>& genes, i
   return rc;
 }
 
+// Progressive SoP MSA of `genes` from the call's pairwise penalties into `path` (FASTA).
+static int write_msa(const char* path, const std::vector<std::string>& genes, const std::string& all,
+                     const std::vector<int64_t>& off, int pxy, int pgap, const std::vector<int32_t>& penalties) {
+  FILE* f = fopen(path, "w");
+  if (!f) return NWK_EINVAL;
+  nwk_ctx* ctx = nullptr;
+  int rc = nwk_ctx_create(nullptr, &ctx);
+  const int64_t cap = off.back() > 0 ? off.back() : 1;
+  std::vector<uint8_t> rows((size_t)cap * (genes.empty() ? 1 : genes.size()));
+  int64_t len = 0, sop = 0;
+  if (rc == NWK_OK)
+    rc = nwk_set_sequences(ctx, reinterpret_cast<const uint8_t*>(all.data()), off.data(), (int32_t)genes.size());
+  if (rc == NWK_OK) rc = nwk_msa(ctx, pxy, pgap, penalties.data(), rows.data(), cap, &len, &sop);
+  for (size_t r = 0; rc == NWK_OK && r < genes.size(); ++r)
+    fprintf(f, ">seq%zu sop=%lld\n%.*s\n", r, (long long)sop, (int)len, (const char*)rows.data() + r * cap);
+  nwk_ctx_destroy(ctx);
+  fclose(f);
+  return rc;
+}
+
 int main(int argc, char** argv) {
   nwk_opts o;
   nwk_opts_default(&o);
   if (const char* g = getenv("NWK_GPUS")) o.ngpus = atoi(g);
   if (const char* v = getenv("NWK_VERBOSE")) o.verbose = atoi(v);
   if (const char* b = getenv("NWK_BITS")) o.bits = atoi(b);
-  const char *fasta = nullptr, *dump = nullptr;
+  const char *fasta = nullptr, *dump = nullptr, *msa = nullptr;
   int fpxy = 3, fpgap = 2;
   for (int a = 1; a < argc; ++a) {
     if (!strcmp(argv[a], "--gpus") && a + 1 < argc) o.ngpus = atoi(argv[++a]);
@@ -94,9 +117,10 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[a], "--pxy") && a + 1 < argc) fpxy = atoi(argv[++a]);
     else if (!strcmp(argv[a], "--pgap") && a + 1 < argc) fpgap = atoi(argv[++a]);
     else if (!strcmp(argv[a], "--dump") && a + 1 < argc) dump = argv[++a];
+    else if (!strcmp(argv[a], "--msa") && a + 1 < argc) msa = argv[++a];
     else {
       fprintf(stderr,
-              "usage: %s [--gpus N] [--bits W] [--verbose] [--fasta FILE --pxy P --pgap G] [--dump FILE] [< input]\n",
+              "usage: %s [--gpus N] [--bits W] [--verbose] [--fasta FILE --pxy P --pgap G] [--dump FILE] [--msa FILE] [< input]\n",
               argv[0]);
       return 2;
     }
@@ -142,6 +166,10 @@ int main(int argc, char** argv) {
   std::cout << std::endl;
   if (dump && (rc = dump_pairs(dump, genes, misMatchPenalty, gapPenalty)) != NWK_OK) {
     fprintf(stderr, "seqalkway: --dump: error %d: %s\n", rc, nwk_last_error());
+    return 1;
+  }
+  if (msa && (rc = write_msa(msa, genes, all, off, misMatchPenalty, gapPenalty, penalties)) != NWK_OK) {
+    fprintf(stderr, "seqalkway: --msa: error %d: %s\n", rc, nwk_last_error());
     return 1;
   }
   return 0;

@@ -462,3 +462,18 @@ def test_linear_space_big13(golden):
         pen, hs = e.align_pairs(_all_ids(len(genes)), pxy, pgap)
     assert [int(v) for v in pen] == c["penalties"]
     assert seqalign.chain_hash(hs) == c["hash"]
+
+
+def test_driver_msa_fasta(golden, tmp_path):
+    """--msa writes the progressive SoP MSA as FASTA; rows and score equal the oracle's; stdout unchanged."""
+    c = golden["mseq1"]
+    text = open(os.path.join(GOLDEN_DIR, "data", c["file"]), "rb").read()
+    pxy, pgap, genes = seqalign.parse_input(text)
+    out_fa = tmp_path / "msa.fa"
+    out = subprocess.run([os.path.join(PKG, "bin", "seqalkway"), "--msa", str(out_fa)], input=text,
+                         stdout=subprocess.PIPE, check=True, timeout=300).stdout.decode().split("\n")
+    assert out[1] == c["hash"] and out[2] == "".join("%d " % p for p in c["penalties"])
+    rows, sop = oracle.msa(genes, pxy, pgap)
+    recs = seqalign.parse_fasta(out_fa.read_bytes())
+    assert recs == rows
+    assert out_fa.read_bytes().split(b"\n")[0] == b">seq0 sop=%d" % sop
