@@ -1868,7 +1868,6 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
         mptr += (8 / SPD) * kRows * kWave;
       }
       if (to_below && sb >= 1 && sb <= pd.nchunks) st_granule(gout + 64 * (sb - 1), a.epoch, stH);
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(pend) :: "memory");
       __builtin_amdgcn_wave_barrier();
       PROG(0x20000000u | ((unsigned)band << 12) | (unsigned)(sb & 0xfff));
     }
