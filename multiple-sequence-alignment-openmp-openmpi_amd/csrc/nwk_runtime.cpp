@@ -811,6 +811,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   // pace of their slowest member; more waves per SIMD only add waiting);
   // NWK_BPC overrides (experiments)
   if (pl.mode == kPacked2) bpc = std::min(bpc, 2);
+  // nw_align_affine: 2 waves/SIMD beat 3 by ~4% kernel GCUPS on big13 and C5
+  // (profiles/r01/ab_affine_bpc.json)
+  if (pl.mode == kAffine) bpc = std::min(bpc, 2);
   static const int bpc_cap = getenv("NWK_BPC") ? atoi(getenv("NWK_BPC")) : 0;
   if (bpc_cap > 0) bpc = std::min(bpc_cap, fill_blocks_per_cu(pl.mode, pl.bits));
   const int grid = bpc * c->cus;
