@@ -1,32 +1,44 @@
 #!/usr/bin/env python3
 """Benchmark: all-pairs Needleman-Wunsch on MI355X, reference metric GCUPS.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload big13|c3|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|big13|c4|c5]
 
-One "step" = the whole getMinimumPenalties job of the workload: every pair's
-fill + traceback + trim + SHA-512 on its rank's GPU/host, the ONE all-gather
-of result records across ranks (N>1, RCCL), and rank 0's hash chain.  Inputs
-(sequences) are resident in HBM before the timed region.  value = total DP
-cells of the job / max-over-ranks wall time per step (strong scaling: the
-workload is fixed, its pairs are LPT-sharded over N GPUs).
+One "step" = the whole getMinimumPenalties job of the workload (skel:117-175,
+sub:232-364): every pair's fill + traceback + trim + SHA-512 on its rank's GPU,
+the ONE all-gather of 72-byte result records across ranks (N>1, RCCL), and
+rank 0's hash chain.  Sequences are resident in HBM before the timed region.
+value = total DP cells of the job / max-over-ranks wall time per step (strong
+scaling: the workload is fixed, its pairs are LPT-sharded over N GPUs).
 
-Default workload = BASELINE.json configs[1]: mseq-big13-example.txt (k=13,
-78 pairs, 2.785e11 cells), the reference's own headline input; its answer
-hash is checked against the published one every run.
+Default workload = C3 (BASELINE.json configs[2]), the configuration the
+north_star target is quoted on: synthetic k=64, L=50,000 ACGT, pxy=3 pgap=2,
+2,016 pairs, 5.04e12 cells.  Its answer hash and penalties are checked in-run
+against tests/golden/large/c3.json (oracle/_ref/sub, the reference's own
+program compiled from its sources, run in the build container).  big13 is
+checked against the reference's published answer (testing3/sequential.txt).
+
+--gpus N without torch.distributed.run: the bench launches N rank processes
+itself (before anything touches the GPU) and fails if N exceeds the visible
+devices; under torch.distributed.run, --gpus must equal WORLD_SIZE.
 
 Also reported (rank 0):
-  roofline      nw_fill (the dominant kernel): algorithmic bytes per launch
-                (4 B per DP cell, the reference's int32 matrix)
-                / the fill launch's duration from HIP events on the engine
-                stream; traffic = PMC-measured HBM bytes per launch when
-                profiles/<round>/pmc_summary.json exists (else null).
+  roofline      the fill kernel (99.5% of GPU time).  Its per-launch duration
+                is measured live (HIP events on the engine stream).  Its
+                per-launch counters -- VALU wave-instructions, GRBM_GUI_ACTIVE,
+                HBM bytes (2 x FETCH_SIZE + WRITE_SIZE) -- come from the
+                rocprofv3 --pmc passes of this same command committed under
+                profiles/<round>/pmc_<workload>.json (tools/pmc_roofline.py).
+                frac is <= 1 for both roofs; "bound" names the larger.
   cpu_baseline  the reference's submitted MPI+OpenMP program (oracle/_ref/sub,
-                compiled from the reference sources) on a bounded sample of
-                the same workload, on this host's cores.
+                compiled from the reference sources) under mpirun on this
+                host, on a labelled prefix subset of the same workload.
 """
 import argparse
+import glob
 import json
 import os
+import shutil
+import socket
 import subprocess
 import sys
 import time
@@ -40,94 +52,203 @@ for p in (PKG, ORACLE):
 
 import numpy as np  # noqa: E402
 
+import workloads  # noqa: E402
+
 METRIC = "DP cell-updates/s (GCUPS) on k-way SoP MSA; 1/2/4/8 MI355X"
-HBM_PEAK_GBS = 8000.0
-BYTES_PER_CELL = 4.0
-
-
-def synth(k, L, seed=0):
-    """Seeded uniform ACGT (mt19937_64-style per-sequence seeds)."""
-    out = []
-    for s in range(k):
-        rng = np.random.Generator(np.random.MT19937(seed + s))
-        out.append(np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, L)].tobytes())
-    return out
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E ~8 TB/s
+SIMDS = 1024                   # 256 CUs x 4 SIMDs
+VALU_CYC_PER_WAVE_INSTR = 2    # MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles
+BYTES_PER_CELL = 4.0           # the reference's int32 matrix (sub:428, 478-487)
+GOLDEN = os.path.join(REPO, "tests", "golden")
 
 
 def load_workload(name):
+    """(description, pxy, pgap, genes, affine, expected answer or None)."""
     import seqalign
 
     if name == "big13":
-        text = open(os.path.join(REPO, "tests", "golden", "data", "mseq-big13-example.txt"), "rb").read()
+        text = open(os.path.join(GOLDEN, "data", "mseq-big13-example.txt"), "rb").read()
         pxy, pgap, genes = seqalign.parse_input(text)
-        gold = {c["name"]: c for c in json.load(open(os.path.join(REPO, "tests", "golden", "golden.json")))["cases"]}
-        return "mseq-big13-example.txt (k=13)", pxy, pgap, genes, gold["big13"]["hash"]
-    if name == "c3":
-        return "synthetic k=64 L=50000 ACGT", 3, 2, synth(64, 50000), None
-    if name == "c4":
-        return "synthetic k=256 L=8000 ACGT", 3, 2, synth(256, 8000), None
-    if name == "c5":  # affine-gap variant (SURVEY §8(d): go=3, ge=1)
-        return "synthetic k=32 L=200000 ACGT, affine go=3 ge=1", 3, 2, synth(32, 200000), None
+        gold = {c["name"]: c for c in json.load(open(os.path.join(GOLDEN, "golden.json")))["cases"]}
+        g = gold["big13"]
+        return "mseq-big13-example.txt (k=13)", pxy, pgap, genes, None, {
+            "hash": g["hash"], "penalties": g["penalties"], "source": g["source"]}
+    if name in workloads.SYNTH:
+        desc, k, L, pxy, pgap, affine = workloads.SYNTH[name]
+        expect = None
+        f = os.path.join(GOLDEN, "large", name + ".json")
+        if os.path.exists(f) and affine is None:
+            g = json.load(open(f))
+            expect = {"hash": g["hash"], "penalties": g["penalties"], "source": g["source"]}
+        return desc, pxy, pgap, workloads.synth(k, L), affine, expect
     raise SystemExit("unknown workload " + name)
 
 
-def cells_of(genes, ids):
-    import seqalign
+# ---------------------------------------------------------------------------
+# CPU baseline: the reference's own program on this host
+# ---------------------------------------------------------------------------
+def host_info():
+    info = {"host_cpus": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except Exception:
+        pass
+    try:
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q[0] != "max":
+            info["cgroup_cpu_quota"] = round(int(q[0]) / int(q[1]), 2)
+    except Exception:
+        pass
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")]
+        sockets = {l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("physical id")}
+        info["cpu_model"] = model[0] if model else None
+        info["sockets"] = len(sockets) or None
+    except Exception:
+        pass
+    return info
 
-    L = [len(g) for g in genes]
-    tot = 0
-    for p in ids:
-        i, j = seqalign.pair_ij(int(p))
-        tot += L[i] * L[j]
-    return tot
+
+def cpu_share():
+    """CPUs this run may use: the box gives one GPU's job a 16-CPU share
+    (OMP_NUM_THREADS=16 there); a cgroup quota or affinity mask below that wins."""
+    share = int(os.environ.get("NWK_BENCH_CPU_SHARE", os.environ.get("OMP_NUM_THREADS", "16")) or 16)
+    hi = host_info()
+    for key in ("affinity_cpus", "cgroup_cpu_quota"):
+        if hi.get(key):
+            share = min(share, int(hi[key]))
+    return max(share, 1), hi
 
 
-def cpu_baseline(genes, pxy, pgap, affine=None):
-    """The CPU path on a bounded sample of the workload (about 10-30 s).
+def cpu_baseline(genes, pxy, pgap, affine=None, budget_s=20.0):
+    """The CPU path on a bounded prefix subset of the workload (~10-30 s).
 
     linear: the reference's submitted program (oracle/_ref/sub, compiled from
-    the reference sources) on the 5 shortest sequences, each cut to at most
-    60k characters (big13: its 5 shortest, 30k-50k, uncut).  Falls back to the
-    single-thread oracle port when the reference binary is absent.
+    submit/xuliny-seqalkway.cpp), R = share // 16 MPI ranks under mpirun (sub
+    hard-codes 16 OpenMP threads per rank, sub:94,238,425), on the first k'
+    sequences of the workload -- exactly its first k'(k'-1)/2 canonical pairs
+    -- with k' sized to ~budget_s at the reference's measured ~0.07 GCUPS/core.
     affine: the reference has no affine path, so the oracle's restatement
-    (single thread) on 3 sequences cut to 8k characters.
+    (single thread, O(n) score-only fill) on one pair cut to fit the budget.
     """
     import oracle
 
+    share, hi = cpu_share()
     if affine:
         go, ge = affine
-        sample = [g[:8000] for g in genes[:3]]
-        cells = sum(len(sample[i]) * len(sample[j]) for i in range(1, 3) for j in range(i))
+        L = int((budget_s * 0.25e9) ** 0.5)
+        x, y = genes[1][:L], genes[0][:L]
         t0 = time.perf_counter()
-        oracle.all_pairs_affine(sample, pxy, go, ge)
+        oracle.score_affine(x, y, pxy, go, ge)
         dt = time.perf_counter() - t0
-        return {"value": round(cells / dt / 1e9, 4), "unit": "GCUPS", "cores": 1, "kind": "port",
-                "sample": "oracle nwo_pair_affine (1 thread) on 3 sequences cut to 8000, %.3g cells" % cells}
-    order = sorted(range(len(genes)), key=lambda i: (len(genes[i]), i))[:5]
-    sample = [genes[i][:60000] for i in sorted(order)]
-    k = len(sample)
-    cells = sum(len(sample[i]) * len(sample[j]) for i in range(1, k) for j in range(i))
-    text = b"%d\n%d\n%d\n" % (pxy, pgap, k) + b"\n".join(sample) + b"\n"
-    desc = "%d shortest sequences (lengths %s), %d pairs, %.3g cells" % (
-        k, ",".join(str(len(s)) for s in sample), k * (k - 1) // 2, cells)
+        return dict({"value": round(len(x) * len(y) / dt / 1e9, 4), "unit": "GCUPS", "cores": 1, "kind": "port",
+                     "sample": "oracle nwo_score_affine (1 thread, score-only) on pair (1,0) cut to %d x %d" % (
+                         len(x), len(y))}, **hi)
+    ranks = max(1, share // 16)
+    est_gcups = 0.07 * 16 * ranks
+    L = np.array([len(g) for g in genes], dtype=np.float64)
+    kk = 2
+    while kk < len(genes) and workloads.cells(genes[:kk + 1]) / (est_gcups * 1e9) <= budget_s:
+        kk += 1
+    sample = genes[:kk]
+    cells = workloads.cells(sample)
+    text = workloads.token_text(pxy, pgap, sample)
+    desc = "first %d sequences of the workload (canonical pairs 0..%d, lengths %d-%d), %.3g cells" % (
+        kk, kk * (kk - 1) // 2 - 1, int(L[:kk].min()), int(L[:kk].max()), cells)
     sub = os.path.join(oracle.REF_DIR, "sub")
+    mpirun = shutil.which("mpirun") or ("/opt/conda/bin/mpirun" if os.path.exists("/opt/conda/bin/mpirun") else None)
     if os.path.exists(sub):
+        cmd = [sub] if ranks == 1 or mpirun is None else [mpirun, "-np", str(ranks), sub]
         try:
-            us, _, _ = oracle.run_cli(sub, text, timeout=600)
-            # sub forces 16 OpenMP threads per rank (sub:94,238,425): 15 compute + 1 master
-            return {"value": round(cells / us / 1e3, 4), "unit": "GCUPS", "cores": 16, "kind": "reference",
-                    "sample": "oracle/_ref/sub (submit/xuliny-seqalkway.cpp, singleton rank, 16 threads) on " + desc,
-                    "host_cpus": os.cpu_count()}
+            r = subprocess.run(cmd, input=text, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=900)
+            if r.returncode != 0:
+                raise RuntimeError("exit %d: %s" % (r.returncode, r.stderr[-300:].decode("latin-1")))
+            lines = r.stdout.decode("latin-1").split("\n")
+            ti = max(i for i, l in enumerate(lines) if l.startswith("Time: "))
+            us = int(lines[ti].split()[1])
+            return dict({"value": round(cells / us / 1e3, 4), "unit": "GCUPS", "cores": 16 * ranks,
+                         "kind": "reference", "ranks": ranks,
+                         "launch": " ".join(os.path.basename(c) for c in cmd),
+                         "sample": "oracle/_ref/sub (submit/xuliny-seqalkway.cpp, %d rank(s) x 16 OpenMP threads; "
+                                   "CPU share of this run = %d) on %s" % (ranks, share, desc),
+                         "answer_hash": lines[ti + 1]}, **hi)
         except Exception as e:  # fall through to the port
-            desc += " [reference binary failed: %s]" % str(e)[:120]
-    # port: the oracle CLI (single-thread restatement of skel) on the 3 shortest, cut to 20k
-    sample = [g[:20000] for g in sample[:3]]
-    k = len(sample)
-    cells = sum(len(sample[i]) * len(sample[j]) for i in range(1, k) for j in range(i))
-    text = b"%d\n%d\n%d\n" % (pxy, pgap, k) + b"\n".join(sample) + b"\n"
-    us, _, _ = oracle.run_cli(oracle.CLI, text, timeout=600)
-    return {"value": round(cells / us / 1e3, 4), "unit": "GCUPS", "cores": 1, "kind": "port",
-            "sample": "oracle/_build/nw_oracle (skel restatement, 1 thread) on %d sequences, %.3g cells" % (k, cells)}
+            desc += " [reference binary failed: %s]" % str(e)[:160]
+    # port: the oracle CLI (single-thread restatement of skel) on the 3 first, cut to 20k
+    sample = [g[:20000] for g in genes[:3]]
+    cells = workloads.cells(sample)
+    us, _, _ = oracle.run_cli(oracle.CLI, workloads.token_text(pxy, pgap, sample), timeout=600)
+    return dict({"value": round(cells / us / 1e3, 4), "unit": "GCUPS", "cores": 1, "kind": "port",
+                 "sample": "oracle/_build/nw_oracle (skel restatement, 1 thread) on 3 sequences cut to 20000 "
+                           "(%.3g cells); %s" % (cells, desc)}, **hi)
+
+
+# ---------------------------------------------------------------------------
+# Roofline: live kernel duration x committed per-launch counters
+# ---------------------------------------------------------------------------
+def load_pmc(workload, kernel):
+    """Newest profiles/r*/pmc_<workload>.json for this kernel (per-launch counters)."""
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_%s.json" % workload)), reverse=True):
+        d = json.load(open(f))
+        if d.get("kernel", "").endswith(kernel):
+            d["_file"] = os.path.relpath(f, REPO)
+            return d
+    return None
+
+
+def roofline(workload, kernel, launch_s, my_cells, launches):
+    pmc = load_pmc(workload, kernel)
+    eq_gbs = my_cells * BYTES_PER_CELL / launches / launch_s / 1e9
+    out = {"kernel": kernel, "launch_ms": round(launch_s * 1e3, 3),
+           "equivalent_4B_per_cell_GBps": round(eq_gbs, 1)}
+    if pmc is None:
+        out.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+                    "note": "no profiles/r*/pmc_%s.json for %s" % (workload, kernel)})
+        return out
+    clk = pmc["grbm_gui_active_per_launch"] / 8.0 / (pmc["duration_ns_per_launch"] * 1e-9)  # Hz, 8 XCDs
+    insts = pmc["sq_insts_valu_per_launch"]
+    valu_frac = insts * VALU_CYC_PER_WAVE_INSTR / SIMDS / (clk * launch_s)
+    valu = {"achieved": round(insts * 64 / launch_s / 1e12, 2),
+            "peak": round(SIMDS * 64 / VALU_CYC_PER_WAVE_INSTR * clk / 1e12, 2),
+            "unit": "Tlane-op/s", "frac": round(valu_frac, 4), "clock_GHz": round(clk / 1e9, 3),
+            "valu_wave_instr_per_launch": insts}
+    traffic = pmc["hbm_bytes_per_launch"]
+    hbm = {"achieved": round(traffic / launch_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(traffic / launch_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic}
+    bound = "valu" if valu["frac"] >= hbm["frac"] else "hbm"
+    top = valu if bound == "valu" else hbm
+    out.update({"bound": bound, "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"],
+                "frac": top["frac"], "traffic": traffic, "valu": valu, "hbm": hbm,
+                "counters_from": pmc["_file"] + " (rocprofv3 --pmc passes of this bench command; "
+                                 "duration measured live here, counters per launch from the passes)"})
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Rank launcher for `bench.py --gpus N` outside torch.distributed.run
+# ---------------------------------------------------------------------------
+def spawn_ranks(n):
+    share = os.environ.get("NWK_BENCH_SHARE_GPU") == "1"
+    if not share:
+        import torch  # device_count() does not initialise the GPU on this image
+
+        vis = torch.cuda.device_count()
+        if n > vis:
+            print("bench.py: --gpus %d but only %d GPU(s) visible" % (n, vis), file=sys.stderr)
+            return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = rc or p.wait()
+    return rc
 
 
 def main():
@@ -135,7 +256,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="big13")
+    ap.add_argument("--workload", default="c3", choices=["c3", "big13", "c4", "c5"])
     ap.add_argument("--bits", type=int, default=0, help="force DP storage width (4/8/16/32)")
     ap.add_argument("--affine", default=None,
                     help="go,ge: run the affine-gap variant (default for --workload c5: 3,1)")
@@ -143,7 +264,11 @@ def main():
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import seqalign
@@ -158,10 +283,13 @@ def main():
         import dist as nwdist
 
         # Test hooks (not used by the driver): NWK_BENCH_BACKEND=gloo and
-        # NWK_BENCH_SHARE_GPU=1 rehearse the N-rank path on a 1-GPU box.
+        # NWK_BENCH_SHARE_GPU=1 run the N-rank path on a 1-GPU box.
         backend = os.environ.get("NWK_BENCH_BACKEND", "nccl")
+        ndev = seqalign.device_count()
         if os.environ.get("NWK_BENCH_SHARE_GPU") == "1":
-            gpu = local % max(1, seqalign.device_count())
+            gpu = local % max(1, ndev)
+        elif local >= ndev:
+            sys.exit("bench.py: rank %d has no GPU (%d visible)" % (local, ndev))
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             torch.cuda.set_device(gpu)
@@ -170,19 +298,21 @@ def main():
         else:
             tdist.init_process_group(backend)
         dist = tdist
+        world = dist.get_world_size()  # n_gpus comes from the communicator
 
-    name, pxy, pgap, genes, gold_hash = load_workload(args.workload)
-    affine = args.affine if args.affine is not None else ("3,1" if args.workload == "c5" else None)
+    name, pxy, pgap, genes, affine, expect = load_workload(args.workload)
+    if args.affine is not None:
+        affine = tuple(int(v) for v in args.affine.split(","))
+    if affine and tuple(affine) != (0, pgap):
+        expect = None  # the reference's answers are for linear gaps (== affine go=0, ge=pgap only)
     if affine:
-        go, ge = (int(v) for v in affine.split(","))
-        if (go, ge) != (0, pgap):
-            gold_hash = None  # the published answers are for linear gaps (== affine go=0, ge=pgap only)
+        go, ge = affine
     k = len(genes)
     P = k * (k - 1) // 2
     lengths = [len(g) for g in genes]
-    total_cells = cells_of(genes, range(P))
+    total_cells = workloads.cells(genes)
     ws = int(float(os.environ.get("NWK_BENCH_WS_GB", "0")) * (1 << 30))  # test hook: per-rank HBM budget
-    eng = seqalign.Engine(device=gpu if world > 1 else 0, bits=args.bits, verbose=args.verbose, workspace_bytes=ws)
+    eng = seqalign.Engine(device=gpu, bits=args.bits, verbose=args.verbose, workspace_bytes=ws)
     eng.set_sequences(genes)  # sequences resident in HBM before timing
     my_ids = seqalign.shard_pairs(lengths, rank, world) if world > 1 else np.arange(P, dtype=np.int64)
 
@@ -208,23 +338,25 @@ def main():
             if torch.cuda.is_available():
                 torch.cuda.synchronize()
 
-    checked = None
+    def check(pen, h):
+        if rank != 0 or expect is None:
+            return None
+        return h == expect["hash"] and [int(v) for v in pen] == expect["penalties"]
+
+    checks = []
     for _ in range(args.warmup):
-        _, h = step()
-        if rank == 0 and gold_hash is not None:
-            checked = h == gold_hash
+        checks.append(check(*step()))
     sync()
     fills, traces = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        _, h = step()
+        pen, h = step()
         st = eng.stats()
         fills.append(st["fill_ms"])
         traces.append(st["traceback_ms"])
     sync()
     dt = time.perf_counter() - t0
-    if rank == 0 and gold_hash is not None:
-        checked = (checked is not False) and h == gold_hash
+    checks.append(check(pen, h))  # the last timed step's answer
     if world > 1:
         import torch
 
@@ -232,26 +364,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
+        dist.destroy_process_group()
+        eng.close()
         return
 
     ms_step = dt / max(args.steps, 1) * 1e3
     gcups = total_cells * args.steps / dt / 1e9
     st = eng.stats()
-    my_cells = cells_of(genes, my_ids)
+    my_cells = workloads.cells(genes, my_ids) if world > 1 else total_cells
     fill_ms = float(np.mean(fills)) if fills else float("nan")
     launches = max(st["fill_launches"], 1)
-    per_launch_ms = fill_ms / launches
-    alg_bytes = my_cells * BYTES_PER_CELL / launches
-    achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(REPO, "profiles", "pmc_summary.json")
-    if os.path.exists(pmc) and world == 1 and not affine:  # measured for the N=1 linear launch
-        try:
-            traffic = json.load(open(pmc)).get(args.workload, {}).get("hbm_bytes_per_fill_launch")
-        except Exception:
-            traffic = None
+    kernel = seqalign.KERNELS.get(st["mode"], "?")
+    answer_ok = None if expect is None else all(c is True for c in checks)
     out = {
         "metric": METRIC,
         "value": round(gcups, 3),
@@ -263,27 +387,31 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "int32",
-        "data": "reference input file (mseq-big13-example.txt)" if args.workload == "big13" else "synthetic",
+        "dtype": "int16x2-relative (int32-exact results, 4-bit mod-16 traceback storage)"
+                 if st["mode"] in (4, 5) else ("int32" if st["bits"] == 32 else
+                                              "int32 (%d-bit mod-2^W traceback storage)" % st["bits"]),
+        "data": "reference input file (mseq-big13-example.txt)" if args.workload == "big13"
+                else "synthetic (seeded MT19937 ACGT, workloads.py)",
         "config": {"workload": name, "pairs": P, "cells": total_cells, "pxy": pxy,
                    "gaps": ("affine go=%d ge=%d" % (go, ge)) if affine else "linear pgap=%d" % pgap,
                    "storage_bits_per_cell": st["bits"], "mode": seqalign.MODES.get(st["mode"]),
-                   "parallelism": "pair-sharded dp%d (LPT), one RCCL all-gather" % world},
-        "answer_hash_ok": checked,
-        "kernel": {"fill_ms": round(fill_ms, 3), "traceback_ms": round(float(np.mean(traces)), 3),
+                   "parallelism": "pair-sharded dp%d (LPT), one all-gather" % world},
+        "answer_hash_ok": answer_ok,
+        "answer_source": expect["source"] if expect else None,
+        "kernel": {"name": kernel, "fill_ms": round(fill_ms, 3), "traceback_ms": round(float(np.mean(traces)), 3),
                    "fill_gcups": round(my_cells / (fill_ms * 1e-3) / 1e9, 2),
                    "fill_launches_per_step": st["fill_launches"], "batches": st["batches"]},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_cell": BYTES_PER_CELL,
-                     "stored_bytes_per_cell": st["bits"] / 8.0},
+        "roofline": roofline(args.workload if not args.affine else args.workload + "_affine", kernel,
+                             fill_ms / launches * 1e-3, my_cells, launches),
     }
-    if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(genes, pxy, pgap, (go, ge) if affine else None)
+    if not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(genes, pxy, pgap, affine)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
     eng.close()
+    if answer_ok is False:
+        sys.exit("bench.py: answer hash / penalties differ from " + expect["source"])
 
 
 if __name__ == "__main__":

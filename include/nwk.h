@@ -60,7 +60,9 @@ typedef struct nwk_opts {
   int32_t finalize;          /* pair finalize (rows, penalty, SHA-512): 0 auto, 1 host, 2 device (nw_hash) */
   int32_t linear_space;      /* linear-space traceback: 0 = only for pairs whose matrix exceeds
                                 the HBM budget, -1 = never, G > 0 = every pair, G bands per recompute group */
-  int32_t reserved[3];
+  int32_t kernel;            /* linear fill kernel: 0 auto, 1 nw_align, 2 nw_align_pk, 3 nw_align_pk2 (a packed
+                                kernel where it is not exact -- W > 4 or mixed-sign K -- falls back to nw_align) */
+  int32_t reserved[2];
 } nwk_opts;
 
 typedef struct nwk_stats {
@@ -186,6 +188,19 @@ int nwk_msa(nwk_ctx *ctx, int32_t pxy, int32_t pgap, const int32_t *penalties, u
  */
 int nwk_shard_pairs(const int64_t *offsets, int32_t k, int32_t rank, int32_t world,
                     int64_t *out_ids, int64_t *out_n);
+
+/*
+ * Host finalize of one traced pair (the step after the GPU traceback): the
+ * prefix fill (skel:263-272), trim (skel:135-154), penalty (the cost of the
+ * traced path, = dp[m][n]) and problemhash (skel:155-157).  moves[0..nmoves)
+ * is the traceback in walk order from (m, n): 'D' diagonal, 'U' up (x_i
+ * against '_'), 'L' left ('_' against y_j); the walk must end on row 0 or
+ * column 0 (NWK_EINVAL otherwise).  a1/a2 need m+n bytes each; problem_hash
+ * gets the 64 raw bytes.  No device is needed.
+ */
+int nwk_finalize_moves(const uint8_t *x, int32_t m, const uint8_t *y, int32_t n, int32_t pxy,
+                       int32_t pgap, const uint8_t *moves, int64_t nmoves, uint8_t *a1, uint8_t *a2,
+                       int32_t *alen, int32_t *penalty, uint8_t *problem_hash);
 
 /* Chain (skel:159): acc = sha512hex(acc ++ hex(problem_hash[p])), p = 0..P-1. */
 int nwk_chain_hash(const uint8_t *problem_hash, int64_t P, char *hash_hex);

@@ -378,9 +378,11 @@ int choose_plan(const nwk_ctx* c, const Scoring& sc, Plan* pl) {
   pl->K0 = (int)(-2 * (int64_t)pgap);
   pl->K1 = (int)((int64_t)pxy - 2 * (int64_t)pgap);
   // two cells per register when the profile bytes sign-extend uniformly
-  // (K0, K1 both < 0 or both >= 0); NWK_PACKED=0 keeps nw_align (A/B)
-  // NWK_PACKED=0 / 1 select nw_align / nw_align_pk instead of the default nw_align_pk2 (A/B)
-  static const int packed = getenv("NWK_PACKED") ? atoi(getenv("NWK_PACKED")) : 2;
+  // (K0, K1 both < 0 or both >= 0).  opts.kernel (or NWK_PACKED=0/1/2 when it is
+  // 0) pins nw_align / nw_align_pk / nw_align_pk2 for tests and A/B runs; a
+  // packed kernel asked for where it is not exact falls back to nw_align.
+  static const int packed_env = getenv("NWK_PACKED") ? atoi(getenv("NWK_PACKED")) : 2;
+  const int packed = c->opts.kernel > 0 ? c->opts.kernel - 1 : packed_env;
   if (pl->mode == kProfile && pl->bits == 4 && packed > 0 && ((pl->K0 < 0) == (pl->K1 < 0)))
     pl->mode = packed == 1 ? kPacked : kPacked2;
   return NWK_OK;
@@ -736,7 +738,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   // (1024 rows, 16 cells per lane-step) too few to occupy the wave slots make
   // each pair's row sweep the critical path -- single bands (nw_align_pk,
   // 8 cells per lane-step) sweep a row in about half the time.
-  if (pl.mode == kPacked2 && !getenv("NWK_PACKED")) {
+  if (pl.mode == kPacked2 && !getenv("NWK_PACKED") && c->opts.kernel == 0) {
     int64_t t2 = 0;
     for (const auto& w : work)
       if (w.m > 0 && w.n > 0) t2 += ceil_div(w.m, 2 * kBandRows);
@@ -1407,6 +1409,36 @@ int nwk_shard_pairs(const int64_t* offsets, int32_t k, int32_t rank, int32_t wor
   return NWK_OK;
 }
 
+int nwk_finalize_moves(const uint8_t* x, int32_t m, const uint8_t* y, int32_t n, int32_t pxy, int32_t pgap,
+                       const uint8_t* moves, int64_t nmoves, uint8_t* a1, uint8_t* a2, int32_t* alen,
+                       int32_t* penalty, uint8_t* problem_hash) {
+  if (m < 0 || n < 0 || nmoves < 0 || (m > 0 && !x) || (n > 0 && !y) || (nmoves > 0 && !moves) || !alen ||
+      !penalty || !problem_hash || ((m > 0 || n > 0) && (!a1 || !a2)))
+    return fail(NWK_EINVAL, "nwk_finalize_moves: bad argument");
+  // walk the moves from (m, n) to where they end, which must be a border cell
+  int64_t i = m, j = n;
+  for (int64_t t = 0; t < nmoves; ++t) {
+    const uint8_t op = moves[t];
+    if (op != 'D' && op != 'U' && op != 'L') return fail(NWK_EINVAL, "nwk_finalize_moves: move %lld is not D/U/L", (long long)t);
+    if (i == 0 || j == 0) return fail(NWK_EINVAL, "nwk_finalize_moves: move %lld leaves the border", (long long)t);
+    i -= op != 'L';
+    j -= op != 'U';
+  }
+  if (i != 0 && j != 0) return fail(NWK_EINVAL, "nwk_finalize_moves: walk ends at (%lld, %lld), off the border", (long long)i, (long long)j);
+  // walk order from (m, n) is the order the kernels emit and finalize_pair takes
+  std::vector<uint8_t> r1, r2;
+  Finalized f;
+  finalize_pair(x, m, y, n, Scoring{pxy, pgap, false, 0, 0}, moves, (int)nmoves, (int)i, (int)j, &f, &r1, &r2);
+  if (!r1.empty()) {
+    memcpy(a1, r1.data(), r1.size());
+    memcpy(a2, r2.data(), r2.size());
+  }
+  *alen = (int32_t)r1.size();
+  *penalty = f.penalty;
+  memcpy(problem_hash, f.hash, 64);
+  return NWK_OK;
+}
+
 int nwk_chain_hash(const uint8_t* ph, int64_t P, char* hash_hex) {
   if (!hash_hex || (P > 0 && !ph)) return fail(NWK_EINVAL, "nwk_chain_hash: bad argument");
   char buf[256];
@@ -1478,6 +1510,30 @@ static int min_penalties_sc(const uint8_t* seqs, const int64_t* offsets, int32_t
   if (ncclCommInitAll(comms.data(), G, devs.data()) != ncclSuccess)
     return fail(NWK_ECOMM, "ncclCommInitAll failed");
   std::vector<ResultRecord> gathered((size_t)per * G);
+  // Collective buffers and streams for every rank are set up here, before any
+  // rank thread starts: either all of them exist and every rank then calls
+  // ncclAllGather exactly once (a rank whose alignment failed still joins with
+  // records tagged -2), or none does and the call fails without a collective.
+  // No rank can be left waiting in the all-gather for a peer that bailed out.
+  std::vector<void*> dsend((size_t)G, nullptr), drecv((size_t)G, nullptr);
+  std::vector<hipStream_t> cstream((size_t)G, nullptr);
+  auto free_coll = [&]() {
+    for (int r = 0; r < G; ++r) {
+      (void)hipSetDevice(r);
+      if (dsend[r]) (void)hipFree(dsend[r]);
+      if (drecv[r]) (void)hipFree(drecv[r]);
+      if (cstream[r]) (void)hipStreamDestroy(cstream[r]);
+    }
+    for (auto& cm : comms) ncclCommDestroy(cm);
+  };
+  for (int r = 0; r < G; ++r) {
+    if (hipSetDevice(r) != hipSuccess || hipMalloc(&dsend[r], sizeof(ResultRecord) * per) != hipSuccess ||
+        hipMalloc(&drecv[r], sizeof(ResultRecord) * per * G) != hipSuccess ||
+        hipStreamCreateWithFlags(&cstream[r], hipStreamNonBlocking) != hipSuccess) {
+      free_coll();
+      return fail(NWK_ENOMEM, "rank %d: collective buffers could not be allocated", r);
+    }
+  }
   std::vector<int> rcs((size_t)G, NWK_OK);
   std::vector<std::string> errs((size_t)G);
   std::vector<std::thread> th;
@@ -1499,34 +1555,28 @@ static int min_penalties_sc(const uint8_t* seqs, const int64_t* offsets, int32_t
         rec[q].penalty = pen[q];
         memcpy(rec[q].hash, hh.data() + 64 * q, 64);
       }
-      // The collective runs even after a local failure (tagged records), so
-      // no rank is left waiting in ncclAllGather.
-      if (rc != NWK_OK) for (auto& x : rec) x.pair_id = -2;
-      (void)hipSetDevice(r);
-      void *dsend = nullptr, *drecv = nullptr;
-      hipStream_t s = nullptr;
-      int crc = NWK_OK;
-      if (hipMalloc(&dsend, sizeof(ResultRecord) * per) != hipSuccess ||
-          hipMalloc(&drecv, sizeof(ResultRecord) * per * G) != hipSuccess || hipStreamCreate(&s) != hipSuccess)
-        crc = NWK_ENOMEM;
-      if (crc == NWK_OK) {
-        if (hipMemcpy(dsend, rec.data(), sizeof(ResultRecord) * per, hipMemcpyHostToDevice) != hipSuccess) crc = NWK_EDEVICE;
-        if (ncclAllGather(dsend, drecv, sizeof(ResultRecord) * per, ncclUint8, comms[r], s) != ncclSuccess)
-          crc = NWK_ECOMM;
-        if (hipStreamSynchronize(s) != hipSuccess) crc = NWK_ECOMM;
-        if (r == 0 && crc == NWK_OK)
-          if (hipMemcpy(gathered.data(), drecv, sizeof(ResultRecord) * per * G, hipMemcpyDeviceToHost) != hipSuccess) crc = NWK_EDEVICE;
+      // Every rank joins the collective exactly once, even after a local
+      // failure (records tagged -2), so no peer is left waiting.
+      if (rc != NWK_OK) {
+        for (auto& x : rec) x.pair_id = -2;
+        errs[r] = g_err;
       }
-      if (dsend) (void)hipFree(dsend);
-      if (drecv) (void)hipFree(drecv);
-      if (s) (void)hipStreamDestroy(s);
-      if (rc != NWK_OK) errs[r] = g_err;
+      (void)hipSetDevice(r);
+      int crc = NWK_OK;
+      if (hipMemcpy(dsend[r], rec.data(), sizeof(ResultRecord) * per, hipMemcpyHostToDevice) != hipSuccess)
+        crc = NWK_EDEVICE;
+      if (ncclAllGather(dsend[r], drecv[r], sizeof(ResultRecord) * per, ncclUint8, comms[r], cstream[r]) != ncclSuccess)
+        crc = NWK_ECOMM;
+      if (hipStreamSynchronize(cstream[r]) != hipSuccess) crc = NWK_ECOMM;
+      if (r == 0 && crc == NWK_OK &&
+          hipMemcpy(gathered.data(), drecv[r], sizeof(ResultRecord) * per * G, hipMemcpyDeviceToHost) != hipSuccess)
+        crc = NWK_EDEVICE;
       rcs[r] = rc != NWK_OK ? rc : crc;
       if (c) nwk_ctx_destroy(c);
     });
   }
   for (auto& t : th) t.join();
-  for (auto& cm : comms) ncclCommDestroy(cm);
+  free_coll();
   for (int r = 0; r < G; ++r)
     if (rcs[r] != NWK_OK) return fail(rcs[r], "rank %d: %s", r, errs[r].empty() ? "collective failed" : errs[r].c_str());
   std::vector<char> have((size_t)P, 0);

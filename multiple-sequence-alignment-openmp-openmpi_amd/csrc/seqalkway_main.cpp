@@ -11,6 +11,8 @@
 //                                   whitespace removed)
 //   --dump FILE                     per pair in canonical order: "i j penalty",
 //                                   then align1 and align2 (trimmed rows) lines
+//   --print-inputs                  parse only (no GPU): k, then "<length> <sha512>"
+//                                   per sequence -- the parser parity hook
 //   --msa FILE                      progressive sum-of-pairs MSA (SURVEY §8 f3,
 //                                   nwk_msa) as FASTA: ">seq<i> sop=<score>"
 //                                   headers, one aligned row per record
@@ -48,7 +50,10 @@ static bool read_fasta(const char* path, std::vector<std::string>* out) {
       any = true;
       continue;
     }
-    if (line.empty() || line[0] == ';') continue;
+    bool blank = true;  // whitespace-only lines ("\r" of a CRLF blank line too) are skipped,
+    for (char ch : line)  // as seqalign.parse_fasta's `not line.strip()`
+      if (!isspace((unsigned char)ch)) { blank = false; break; }
+    if (blank || line[0] == ';') continue;
     if (!any) {  // sequence text before the first header: an unnamed record
       out->emplace_back();
       any = true;
@@ -108,6 +113,7 @@ int main(int argc, char** argv) {
   if (const char* v = getenv("NWK_VERBOSE")) o.verbose = atoi(v);
   if (const char* b = getenv("NWK_BITS")) o.bits = atoi(b);
   const char *fasta = nullptr, *dump = nullptr, *msa = nullptr;
+  bool print_inputs = false;
   int fpxy = 3, fpgap = 2;
   for (int a = 1; a < argc; ++a) {
     if (!strcmp(argv[a], "--gpus") && a + 1 < argc) o.ngpus = atoi(argv[++a]);
@@ -118,9 +124,10 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[a], "--pgap") && a + 1 < argc) fpgap = atoi(argv[++a]);
     else if (!strcmp(argv[a], "--dump") && a + 1 < argc) dump = argv[++a];
     else if (!strcmp(argv[a], "--msa") && a + 1 < argc) msa = argv[++a];
+    else if (!strcmp(argv[a], "--print-inputs")) print_inputs = true;
     else {
       fprintf(stderr,
-              "usage: %s [--gpus N] [--bits W] [--verbose] [--fasta FILE --pxy P --pgap G] [--dump FILE] [--msa FILE] [< input]\n",
+              "usage: %s [--gpus N] [--bits W] [--verbose] [--fasta FILE --pxy P --pgap G] [--dump FILE] [--msa FILE] [--print-inputs] [< input]\n",
               argv[0]);
       return 2;
     }
@@ -141,6 +148,15 @@ int main(int argc, char** argv) {
     if (k < 0) k = 0;
     genes.resize((size_t)k);
     for (int i = 0; i < k; i++) std::cin >> genes[i];
+  }
+  if (print_inputs) {
+    printf("%d\n", k);
+    for (auto& g : genes) {
+      char hx[NWK_HASH_HEX];
+      nwk_sha512_hex(reinterpret_cast<const uint8_t*>(g.data()), (int64_t)g.size(), hx);
+      printf("%zu %s\n", g.size(), hx);
+    }
+    return 0;
   }
   std::vector<int64_t> off((size_t)k + 1, 0);
   for (int i = 0; i < k; i++) off[i + 1] = off[i] + (int64_t)genes[i].size();

@@ -9,6 +9,11 @@ ranks are collected with ONE all_gather_into_tensor (backend "nccl" = RCCL
 over xGMI on MI355X; "gloo" in the CPU tests).  Every rank then holds the
 penalties and problem hashes in canonical order; rank 0 runs the sequential
 hash chain (sub:334-337).
+
+Failure contract (the C++ in-process path tags records the same way): a rank
+whose alignment raises still contributes its block, every record tagged
+FAILED, to the one collective; every rank then raises RankFailed instead of
+some ranks hanging in the all-gather.
 """
 import numpy as np
 import torch
@@ -35,10 +40,23 @@ def pack_records(ids, penalties, hashes, per):
     return rec
 
 
+FAILED = -2  # pair_id of every record of a rank whose alignment failed
+
+
+class RankFailed(RuntimeError):
+    pass
+
+
 def unpack_records(gathered, P):
-    """Canonical-order penalties int32[P] and raw hashes uint8[P,64]."""
+    """Canonical-order penalties int32[P] and raw hashes uint8[P,64].
+    Raises RankFailed on every rank when some rank contributed FAILED records."""
     g = np.ascontiguousarray(gathered, dtype=np.uint8).reshape(-1, REC)
     head = g[:, :8].copy().view(np.int32).reshape(-1, 2)
+    if (head[:, 0] == FAILED).any():
+        per = g.shape[0]
+        bad = sorted({r for r in range(per) if head[r, 0] == FAILED})
+        raise RankFailed("all-gather: a rank failed to align its shard (records %d..%d tagged %d)"
+                         % (bad[0], bad[-1], FAILED))
     pen = np.zeros(P, dtype=np.int32)
     hs = np.zeros((P, 64), dtype=np.uint8)
     seen = np.zeros(P, dtype=bool)
@@ -74,8 +92,16 @@ def align_sharded(align_fn, lengths, pxy, pgap, rank, world, device=None, group=
     P = k * (k - 1) // 2
     ids = seqalign.shard_pairs(lengths, rank, world)
     per = max(shard_sizes(lengths, world) + [1])
-    pen, hs = align_fn(ids, pxy, pgap)
-    rec = pack_records(ids, pen, hs, per)
+    err = None
+    try:
+        pen, hs = align_fn(ids, pxy, pgap)
+        rec = pack_records(ids, pen, hs, per)
+    except Exception as e:  # still join the ONE collective, so no peer waits forever
+        err = e
+        rec = pack_records([], [], [], per)
+        rec[:, :4] = np.array([FAILED], dtype=np.int32).view(np.uint8)
     g = all_gather_records(rec, device=device, group=group)
+    if err is not None:
+        raise RankFailed("rank %d: %s" % (rank, err)) from err
     pen_all, hs_all = unpack_records(g, P)
     return pen_all, hs_all, ids

@@ -24,6 +24,8 @@ LIB_PATH = os.path.join(HERE, "lib", "libnwk.so")
 NWK_OK = 0
 ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "EKERNEL", -5: "ECOMM"}
 MODES = {0: "profile", 1: "compare", 2: "literal", 3: "affine", 4: "packed-profile", 5: "packed-band-pairs"}
+# fill kernel of each mode (csrc/nwk_kernels.hip), as rocprofv3 names it
+KERNELS = {0: "nw_align", 1: "nw_align", 2: "nw_align", 3: "nw_align_affine", 4: "nw_align_pk", 5: "nw_align_pk2"}
 
 
 class NwkError(RuntimeError):
@@ -36,7 +38,7 @@ class Opts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("ngpus", ctypes.c_int32), ("bits", ctypes.c_int32),
                 ("host_threads", ctypes.c_int32), ("workspace_bytes", ctypes.c_int64),
                 ("verbose", ctypes.c_int32), ("finalize", ctypes.c_int32),
-                ("linear_space", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
+                ("linear_space", ctypes.c_int32), ("kernel", ctypes.c_int32), ("reserved", ctypes.c_int32 * 2)]
 
 
 class Stats(ctypes.Structure):
@@ -70,6 +72,7 @@ SIGNATURES = {
     "nwk_msa": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _I64, _P, _P]),
     "nwk_shard_pairs": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
     "nwk_chain_hash": (ctypes.c_int, [_P, _I64, _P]),
+    "nwk_finalize_moves": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P]),
     "nwk_sha512_hex": (None, [_P, _I64, _P]),
 }
 
@@ -142,8 +145,10 @@ class Engine:
 
     FINALIZE = {"auto": 0, "host": 1, "device": 2}
 
+    KERNEL = {"auto": 0, "nw_align": 1, "nw_align_pk": 2, "nw_align_pk2": 3}
+
     def __init__(self, device=0, bits=0, workspace_bytes=0, host_threads=0, verbose=False, finalize="auto",
-                 linear_space=0):
+                 linear_space=0, kernel="auto"):
         """finalize: where rows, penalty and SHA-512 of each pair are computed --
         "auto" (per batch, by estimated cost), "host" threads, or "device" (nw_hash)."""
         self.lib = load_library()
@@ -155,6 +160,8 @@ class Engine:
         # linear-space traceback: 0 only where the matrix does not fit,
         # -1 never, G > 0 every pair with G bands per recompute group
         o.linear_space = linear_space
+        # linear fill kernel (tests / A/B): "auto", "nw_align", "nw_align_pk", "nw_align_pk2"
+        o.kernel = self.KERNEL[kernel]
         self._ctx = ctypes.c_void_p()
         _check(self.lib.nwk_ctx_create(ctypes.byref(o), ctypes.byref(self._ctx)))
         self.k = 0
@@ -264,6 +271,39 @@ def chain_hash(problem_hashes):
     out = ctypes.create_string_buffer(129)
     _check(lib.nwk_chain_hash(_ptr(h), h.shape[0], out))
     return out.value.decode()
+
+
+def finalize_moves(x, y, pxy, pgap, moves):
+    """Host finalize (skel:263-272 prefix, 135-157 trim/rows/hash) of a traceback
+    given as moves in walk order from (m, n): (penalty, align1, align2, raw problemhash)."""
+    lib = load_library()
+    xb, yb, mv = _as_bytes(x), _as_bytes(y), _as_bytes(moves)
+    cap = max(len(xb) + len(yb), 1)
+    a1 = ctypes.create_string_buffer(cap)
+    a2 = ctypes.create_string_buffer(cap)
+    alen, pen = ctypes.c_int32(), ctypes.c_int32()
+    ph = ctypes.create_string_buffer(64)
+    _check(lib.nwk_finalize_moves(xb, len(xb), yb, len(yb), pxy, pgap, mv, len(mv), a1, a2, ctypes.byref(alen),
+                                  ctypes.byref(pen), ph))
+    return pen.value, a1.raw[:alen.value], a2.raw[:alen.value], ph.raw
+
+
+def moves_of(a1, a2, m, n):
+    """Walk-order moves (from (m, n)) of an alignment's rows: the inverse of the
+    finalize, for tests.  Columns are read back to front; the prefix run (one
+    row exhausted) is not part of the walk."""
+    out = bytearray()
+    i, j = m, n
+    for c1, c2 in zip(reversed(a1), reversed(a2)):
+        if i == 0 or j == 0:
+            break
+        if c1 != ord("_") and c2 != ord("_"):
+            out.append(ord("D")); i -= 1; j -= 1
+        elif c2 == ord("_"):
+            out.append(ord("U")); i -= 1
+        else:
+            out.append(ord("L")); j -= 1
+    return bytes(out)
 
 
 def sha512_hex(data):

@@ -272,6 +272,71 @@ int nwo_pair_affine(const unsigned char *x, int m, const unsigned char *y, int n
   return ret;
 }
 
+/* ------------------------------------------------------------------------ */
+/* Score-only fills in O(n) memory: dp[m][n] of nwo_pair (skel:195-226) and  */
+/* H[m][n] of nwo_pair_affine, for pairs whose full matrix does not fit the  */
+/* host (C5: 200k x 200k).  Same recurrences row by row; no traceback.       */
+/* Return INT32_MIN if the row buffers cannot be allocated.                  */
+/* ------------------------------------------------------------------------ */
+int nwo_score(const unsigned char *x, int m, const unsigned char *y, int n, int pxy, int pgap) {
+  int *row = (int *)malloc(sizeof(int) * ((size_t)n + 1));
+  if (!row) return INT32_MIN;
+  for (int j = 0; j <= n; ++j) row[j] = j * pgap; /* skel:205-208 */
+  for (int i = 1; i <= m; ++i) {
+    const unsigned char xi = x[i - 1];
+    int diag = row[0], left = i * pgap; /* skel:201-204 */
+    row[0] = left;
+    for (int j = 1; j <= n; ++j) {
+      int up = row[j], v;
+      if (xi == y[j - 1]) {
+        v = diag;
+      } else {
+        v = diag + pxy;
+        if (up + pgap < v) v = up + pgap;
+        if (left + pgap < v) v = left + pgap;
+      }
+      diag = up;
+      row[j] = left = v;
+    }
+  }
+  int ret = row[n];
+  free(row);
+  return ret;
+}
+
+int nwo_score_affine(const unsigned char *x, int m, const unsigned char *y, int n, int pxy, int go, int ge) {
+  int *H = (int *)malloc(sizeof(int) * ((size_t)n + 1)), *F = (int *)malloc(sizeof(int) * ((size_t)n + 1));
+  if (!H || !F) { free(H); free(F); return INT32_MIN; }
+  H[0] = 0;
+  F[0] = NWO_INF;
+  for (int j = 1; j <= n; ++j) { H[j] = go + j * ge; F[j] = NWO_INF; }
+  for (int i = 1; i <= m; ++i) {
+    const unsigned char xi = x[i - 1];
+    int diag = H[0], left = go + i * ge, e = NWO_INF;
+    H[0] = left;
+    for (int j = 1; j <= n; ++j) {
+      int eo = left + go + ge, ee = e + ge;
+      e = eo < ee ? eo : ee;
+      int fo = H[j] + go + ge, fe = F[j] + ge;
+      int f = fo < fe ? fo : fe;
+      int h;
+      if (xi == y[j - 1]) {
+        h = diag;
+      } else {
+        h = diag + pxy;
+        if (f < h) h = f;
+        if (e < h) h = e;
+      }
+      diag = H[j];
+      F[j] = f;
+      H[j] = left = h;
+    }
+  }
+  int ret = H[n];
+  free(H); free(F);
+  return ret;
+}
+
 /* skel:155-157: problemhash = sha512(sha512(a1) ++ sha512(a2)), hex. */
 void nwo_problem_hash(const unsigned char *a1, const unsigned char *a2, int alen, char out[129]) {
   char buf[257];

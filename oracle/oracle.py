@@ -40,6 +40,10 @@ def lib():
         L.nwo_chain.argtypes = [P, ctypes.c_long, P]
         L.nwo_all.restype = ctypes.c_int
         L.nwo_all.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P]
+        L.nwo_score.restype = ctypes.c_int
+        L.nwo_score.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.nwo_score_affine.restype = ctypes.c_int
+        L.nwo_score_affine.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.nwo_sha512_hex.restype = None
         L.nwo_sha512_hex.argtypes = [P, ctypes.c_size_t, P]
         _lib = L
@@ -61,6 +65,24 @@ def pair(x, y, pxy, pgap):
     if pen == -2 ** 31:
         raise MemoryError("oracle: DP allocation failed")
     return pen, a1.raw[:alen.value], a2.raw[:alen.value]
+
+
+def score(x, y, pxy, pgap):
+    """dp[m][n] of skel's fill (skel:195-226) in O(n) memory, no traceback."""
+    x, y = _b(x), _b(y)
+    v = lib().nwo_score(x, len(x), y, len(y), pxy, pgap)
+    if v == -2 ** 31:
+        raise MemoryError("oracle: row allocation failed")
+    return v
+
+
+def score_affine(x, y, pxy, go, ge):
+    """H[m][n] of the affine variant in O(n) memory, no traceback."""
+    x, y = _b(x), _b(y)
+    v = lib().nwo_score_affine(x, len(x), y, len(y), pxy, go, ge)
+    if v == -2 ** 31:
+        raise MemoryError("oracle: row allocation failed")
+    return v
 
 
 def pair_affine(x, y, pxy, go, ge):

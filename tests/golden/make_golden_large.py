@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""Full-size golden answers for BASELINE configs C3/C4/C5 and the int16-range
+edge sets -- written to tests/golden/large/<name>.json, one file per job.
+
+Run in the build container (after oracle/build_ref.sh); each job is
+independent and can run concurrently:
+
+    python tests/golden/make_golden_large.py c3        # sub, ~75 min on 8 cores
+    python tests/golden/make_golden_large.py c3_pairs  # skel_debug, first 9 seqs (36 pairs)
+    python tests/golden/make_golden_large.py c4 c4_pairs
+    python tests/golden/make_golden_large.py edge16    # skel_debug, 4 penalty pairs
+    python tests/golden/make_golden_large.py c5_scores # oracle score-only, O(n) memory
+
+Sources of truth:
+  * "sub"         oracle/_ref/sub = submit/xuliny-seqalkway.cpp compiled from
+                  the reference sources, singleton MPI rank (16 OpenMP threads);
+                  the answer hash and the penalties line (sub:57-69, 334-337).
+  * "skel_debug"  oracle/_ref/skel_debug = root seqalign-mpi-skeleton.cpp; its
+                  debug prints (skel:158-169) give each pair's penalty and
+                  problemhash.  The first 9 sequences of a config give exactly
+                  its first 36 canonical pairs (i < 9).
+  * "oracle score" oracle.score_affine / oracle.score (nw_oracle.c, O(n) memory):
+                  C5 has no reference, so its pin is the oracle's
+                  restatement of the build-defined recurrence.
+
+Inputs are NOT stored: the GPU tests regenerate them bit-for-bit from
+multiple-sequence-alignment-openmp-openmpi_amd/workloads.py (synth) and
+tests/golden/gen_inputs.py (edge16).
+"""
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "multiple-sequence-alignment-openmp-openmpi_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(0, HERE)
+
+import gen_inputs  # noqa: E402
+import oracle  # noqa: E402
+import workloads  # noqa: E402
+from make_golden import run_skel  # noqa: E402
+
+OUT = os.path.join(HERE, "large")
+
+
+def save(name, entry):
+    os.makedirs(OUT, exist_ok=True)
+    entry["name"] = name
+    with open(os.path.join(OUT, name + ".json"), "w") as f:
+        json.dump(entry, f, indent=0)
+    print(name, "written", file=sys.stderr)
+
+
+def run_sub(genes, pxy, pgap):
+    text = workloads.token_text(pxy, pgap, genes)
+    us, h, pens = oracle.run_cli(os.path.join(oracle.REF_DIR, "sub"), text, timeout=6 * 3600)
+    return us, h, pens
+
+
+def job_full(cfg):
+    desc, k, L, pxy, pgap, _ = workloads.SYNTH[cfg]
+    genes = workloads.synth(k, L)
+    us, h, pens = run_sub(genes, pxy, pgap)
+    save(cfg, {"config": desc, "k": k, "L": L, "pxy": pxy, "pgap": pgap, "hash": h, "penalties": pens,
+               "source": "oracle/_ref/sub (submit/xuliny-seqalkway.cpp, singleton rank, 16 threads, "
+                         "8-core build container): %d us" % us})
+
+
+def job_pairs(cfg, nseq=9):
+    desc, k, L, pxy, pgap, _ = workloads.SYNTH[cfg]
+    genes = workloads.synth(nseq, L)
+    h, pens, pairs = run_skel(workloads.token_text(pxy, pgap, genes).decode("latin-1"), debug=True,
+                              timeout=6 * 3600)
+    save(cfg + "_pairs", {"config": desc + " -- first %d sequences (canonical pairs 0..%d)" % (nseq, len(pens) - 1),
+                          "k": nseq, "L": L, "pxy": pxy, "pgap": pgap, "hash": h, "penalties": pens, "pairs": pairs,
+                          "source": "oracle/_ref/skel_debug (root seqalign-mpi-skeleton.cpp, skel:158-169)"})
+
+
+def job_edge16():
+    cases = []
+    for pxy, pgap in gen_inputs.EDGE16_PENALTIES:
+        genes = gen_inputs.edge16_genes(pxy, pgap)
+        t0 = time.time()
+        h, pens, pairs = run_skel(workloads.token_text(pxy, pgap, genes).decode("latin-1"), debug=True,
+                                  timeout=6 * 3600)
+        cases.append({"pxy": pxy, "pgap": pgap, "lengths": [len(g) for g in genes], "hash": h,
+                      "penalties": pens, "pairs": pairs})
+        print("edge16", pxy, pgap, "%.0fs" % (time.time() - t0), file=sys.stderr)
+    save("edge16", {"cases": cases, "source": "oracle/_ref/skel_debug (root seqalign-mpi-skeleton.cpp)",
+                    "generator": "tests/golden/gen_inputs.py edge16_genes"})
+
+
+def job_c5_scores():
+    desc, k, L, pxy, pgap, (go, ge) = workloads.SYNTH["c5"]
+    genes = workloads.synth(k, L)
+    out = []
+    for p, (i, j) in enumerate([(1, 0), (2, 0)]):
+        t0 = time.time()
+        a = oracle.score_affine(genes[i], genes[j], pxy, go, ge)
+        lin = oracle.score(genes[i], genes[j], pxy, pgap)
+        out.append({"pair": p, "i": i, "j": j, "affine_penalty": a, "linear_penalty": lin})
+        print("c5 pair", p, a, lin, "%.0fs" % (time.time() - t0), file=sys.stderr)
+    save("c5_scores", {"config": desc, "pxy": pxy, "pgap": pgap, "go": go, "ge": ge, "scores": out,
+                       "source": "oracle nwo_score_affine / nwo_score (O(n)-memory restatement; the "
+                                 "affine variant has no reference, SURVEY §8 a9)"})
+
+
+def main(argv):
+    for a in argv or ["c3", "c3_pairs", "c4", "c4_pairs", "edge16", "c5_scores"]:
+        if a in ("c3", "c4"):
+            job_full(a)
+        elif a in ("c3_pairs", "c4_pairs"):
+            job_pairs(a[:2])
+        elif a == "edge16":
+            job_edge16()
+        elif a == "c5_scores":
+            job_c5_scores()
+        else:
+            raise SystemExit("unknown job " + a)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -83,3 +83,51 @@ def test_gloo_sharded_gather_matches_golden(world):
     for c in CASES:
         k = len(case_input(c)[2])
         assert per_case[c["name"]] == k * (k - 1) // 2
+
+
+def _failing_worker(rank, world, port, genes, q):
+    import sys
+
+    for p in (PKG, ORACLE):
+        sys.path.insert(0, p)
+    import numpy as np
+
+    import dist as nwdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def align_fn(ids, pxy, pgap):
+            if rank == 1:
+                raise RuntimeError("injected NWK_EKERNEL on rank 1")
+            return np.zeros(len(ids), dtype=np.int32), np.zeros((len(ids), 64), dtype=np.uint8)
+
+        try:
+            nwdist.align_sharded(align_fn, [len(g) for g in genes], 3, 2, rank, world)
+            q.put((rank, "returned"))
+        except nwdist.RankFailed as e:
+            q.put((rank, "raised: %s" % e))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_failing_rank_raises_everywhere(world):
+    """One rank's aligner raises: it still joins the ONE all-gather with
+    records tagged FAILED, and every rank raises RankFailed (none hangs)."""
+    genes = [b"ACGT" * 5, b"AC" * 7, b"GATTACA", b"T" * 11, b"CAT" * 4]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, genes, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(out) == list(range(world))
+    for r, msg in out.items():
+        assert msg.startswith("raised:"), (r, msg)
+    assert "injected" in out[1]
