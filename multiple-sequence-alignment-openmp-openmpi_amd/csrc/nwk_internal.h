@@ -25,6 +25,7 @@ enum Mode : int {
   kPacked = 4,   // kProfile at W = 4 with two cells per register (int16 pairs), packed layout
   kPacked2 = 5,  // kPacked with two bands per wave (band pairs), layout LY 2
   kProfileDP = 6,  // profile-profile sum-of-pairs DP of the progressive MSA, 4-bit codes
+  kAffinePk = 7,   // kAffine on band pairs as int16 pairs (nw_align_pka), layout LY 2, profile codes
 };
 
 // One pair of the batch.  All offsets are element offsets into the

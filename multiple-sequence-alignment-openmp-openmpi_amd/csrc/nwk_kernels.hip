@@ -1744,6 +1744,415 @@ __global__ __launch_bounds__(256) void nw_align_affine(FillArgs a) {
 }
 
 // ===========================================================================
+// Packed affine fill (kAffinePk, nw_align_pka): the Gotoh recurrence of
+// SURVEY §8 a9 on band pairs as int16 pairs -- nw_align_pk2's layout, skew and
+// hand-off (bands 2p / 2p+1 in the low / high halves, the odd band 64 columns
+// behind, one HBM hand-off per 1024 rows) with nw_align_affine's state: E per
+// row in registers, F passed down the rows (across lanes by DPP), two boundary
+// rows (H and F) per band pair.
+//
+// Values are H-space (no relabelling: K = 0 on a match and pxy otherwise, so
+// every profile byte is >= 0), scaled by 4 with a 2-bit tag in the low bits,
+// relative to a per-half wave-uniform base and biased by kPkaBias so both
+// halves stay inside [0, 32767].  Then a 32-bit v_add_u32 adds a packed
+// constant (or the profile word) to both halves with no carry between them --
+// one full-rate instruction instead of a half-rate v_pk_add_u16 -- and
+// v_pk_min_i16 still compares correctly.  The tags make one min yield a value
+// and its source, ties going the oracle's way (nwo_pair_affine):
+//   E = min(4(H_left + go + ge) | 0, E_left' + 4ge),  E' = E | 3   (open 0 < extend 3)
+//   F = min(4(H_up   + go + ge) | 0, F_up'   + 4ge),  F' = F | 1   (open 0 < extend 1)
+//   H = min(4(H_diag + K)       | 0, F', E')  ->  tag 0 D, 1 F, 3 E  (D > F > E)
+// (for pxy, go, ge >= 0 the reference's match shortcut H = H_diag IS that
+// minimum with tag 0: H_diag <= E, F on a match).  The 4-bit
+// code stored per cell: bits 1:0 = H's tag, bit 2 = F extended, bit 3 = E
+// extended; trace_pair_pka walks it.  The host admits a call only when the
+// values provably stay inside the int16 window (pka_admissible, nwk_runtime).
+// ===========================================================================
+constexpr int kPkaBias = 16000;  // scaled value of a half's base (a multiple of 4)
+constexpr int kPkaInf = 32000;   // scaled +inf: E at column 0, F above row 1
+
+__device__ __forceinline__ unsigned pk_or(unsigned a, unsigned m) { return a | m; }
+
+// Eight wavefront steps s0..s0+7 (s0 % 8 == 0).
+//   Hc, Ec: per row, H (tag-clean) and E' of the previous step; Nb: its codes
+//   F7:     row 7's F' of the previous step (lane t+1's row-0 F-up, publish)
+//   bH, bF: LDS rings of the band-above H and F' rows (scaled, low 16 bits)
+//   hb0:    packed border H of row 0 (masked steps), + r * ge4 for row r
+template <bool MASK>
+__device__ __forceinline__ void step_block_pka(int s0, int lane, unsigned (&Hc)[kRows], unsigned (&Ec)[kRows],
+                                               unsigned (&Nb)[kRows], unsigned& F7, unsigned& U, unsigned& stH,
+                                               unsigned& stF, const unsigned (&pl)[kRows], const unsigned (&ph)[kRows],
+                                               const unsigned* srow, const int* bH, const int* bF, unsigned upsel,
+                                               unsigned* mptr, bool pub, u64* gpH, u64* gpF, unsigned epoch,
+                                               int base_hi, unsigned goe4, unsigned ge4, unsigned hb0) {
+  const int4 hA = *reinterpret_cast<const int4*>(bH), hB = *reinterpret_cast<const int4*>(bH + 4);
+  const int4 fA = *reinterpret_cast<const int4*>(bF), fB = *reinterpret_cast<const int4*>(bF + 4);
+  const int bh[8] = {hA.x, hA.y, hA.z, hA.w, hB.x, hB.y, hB.z, hB.w};
+  const int bf[8] = {fA.x, fA.y, fA.z, fA.w, fB.x, fB.y, fB.z, fB.w};
+  unsigned sel[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sel[k] = srow[k];
+  unsigned Xa[kRows];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    // lane 63's {row 7 of band 2p, row 7 of band 2p+1} (previous step) enter the publish windows
+    stH = (unsigned)__builtin_amdgcn_update_dpp((int)Hc[kRows - 1], (int)stH, 0x130 /*wave_shl:1*/, 0xf, 0xf, false);
+    stF = (unsigned)__builtin_amdgcn_update_dpp((int)F7, (int)stF, 0x130, 0xf, 0xf, false);
+    if (k == 7 && pub) {
+      st_granule(gpH, epoch, (int)((stH >> 16) >> 2) - kPkaBias / 4 + base_hi);
+      st_granule(gpF, epoch, (int)((stF >> 16) >> 2) - kPkaBias / 4 + base_hi);
+    }
+    // row 0's up: lane t-1's row 7 (previous step); lane 0: {band above, lane 63's band-2p row 7}
+    const unsigned xH = (unsigned)__builtin_amdgcn_update_dpp(0, (int)Hc[kRows - 1], 0x13c /*wave_ror:1*/, 0xf, 0xf, false);
+    const unsigned xF = (unsigned)__builtin_amdgcn_update_dpp(0, (int)F7, 0x13c, 0xf, 0xf, false);
+    unsigned hup = __builtin_amdgcn_perm(xH, (unsigned)bh[k], upsel);
+    unsigned fup = __builtin_amdgcn_perm(xF, (unsigned)bf[k], upsel);
+    unsigned hdg = U;
+    U = hup;
+    unsigned sk = sel[k];
+    asm volatile("" : "+v"(sk));
+    unsigned Hn[kRows], En[kRows], Nn[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      const unsigned K = __builtin_amdgcn_perm(ph[r], pl[r], sk);  // {4K(x_lo, y), 4K(x_hi, y')}, K >= 0
+      const unsigned dc = hdg + K;                                  // no carry: both halves < 32768
+      const unsigned e = pk_min(Hc[r] + goe4, Ec[r] + ge4);
+      const unsigned f = pk_min(hup + goe4, fup + ge4);
+      const unsigned ec = pk_or(e, 0x00030003u), fc = pk_or(f, 0x00010001u);
+      const unsigned g = pk_min(pk_min(dc, ec), fc);
+      const unsigned hn = g & 0xfffcfffcu;
+      // code: H's tag | F extended << 2 | E extended << 3 (two v_bfi_b32: bit 0 of
+      // f's tag is "extended", and so is bit 1 of e's tag 3; bits 4+ are junk)
+      const unsigned ext = (f & 0x00010001u) | (e & ~0x00010001u);
+      Nn[r] = (g & 0x00030003u) | ((ext << 2) & ~0x00030003u);
+      hdg = Hc[r];
+      hup = hn;
+      fup = fc;
+      Hn[r] = hn;
+      En[r] = ec;
+    }
+    if constexpr (MASK) {  // columns <= 0 keep the border: H = go + i ge, E = +inf
+      const int s = s0 + k;
+      const unsigned M = s >= lane + 64 ? 0xffffffffu : (s >= lane ? 0x0000ffffu : 0u);
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) {
+        const unsigned hb = hb0 + (unsigned)r * ge4;
+        Hn[r] = (Hn[r] & M) | (hb & ~M);
+        En[r] = (En[r] & M) | ((unsigned)(kPkaInf | 3) * 0x10001u & ~M);
+      }
+    }
+    F7 = fup;
+    if (k & 1) {
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) {
+        const unsigned X = __builtin_amdgcn_perm(Nn[r], Nb[r], 0x06040200u);
+        if ((k & 3) == 1) {
+          Xa[r] = X;
+        } else {
+          const unsigned D = (Xa[r] & 0x0f0f0f0fu) | ((X << 4) & 0xf0f0f0f0u);
+          __builtin_nontemporal_store(D, mptr + ((k >> 2) * kRows + r) * kWave);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      Hc[r] = Hn[r];
+      Ec[r] = En[r];
+      Nb[r] = Nn[r];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Traceback of one pair on nw_align_pka's codes (layout LY 2), the same LDS
+// tile staging as trace_pair and the three-state walk of trace_pair_affine:
+// 'D', 'U'/'L' (gap extended) and 'u'/'l' (the gap's first column).
+__device__ __forceinline__ void trace_pair_pka(const FillArgs& a, const PairDesc& pd, TbLds<4, 2>& L, int lane) {
+  using C = TbConf<4, 2>;
+  using Y = Lay<4, 2>;
+  constexpr int SPC = Y::SPC, RPC = Y::RPC;
+  const int64_t bdw = band_dwords(4, pd.sblocks);
+  const int ncols = 64 * pd.sblocks / SPC;
+  const unsigned* mb = a.mat + pd.mat_off;
+  const int lane_off = (lane >> 4) * kWave + (lane & 15);
+  auto issue = [&](int b, int q, int t0) {
+    const unsigned* src = mb + Y::base(b, bdw) + t0 + lane_off;
+#pragma unroll
+    for (int k = 0; k < C::TILE / 64; ++k) {
+      int c = C::TC * q - C::OV + k / (RPC / 4);
+      c = c < 0 ? 0 : (c >= ncols ? ncols - 1 : c);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (int64_t)c * (RPC * kWave) + 4 * (k % (RPC / 4)) * kWave),
+                                       (lds_void*)&L.tile[0][64 * k], 4, 0, 0);
+    }
+  };
+  auto drain = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+  uint8_t* ops = a.ops + pd.ops_off;
+  int i = pd.m, j = pd.n, Lc = 0, flushed = 0, tb = -1, tq = 0, tt0 = 0;
+  unsigned st = 0;  // 0 = H, 1 = F, 2 = E
+  bool bad = false;
+  const unsigned ob = lds_addr(&L.obuf[0]);
+  auto flush = [&](int upto) {
+    const int from = flushed & ~3;
+    for (int o = from + 4 * lane; o < upto; o += 256) {
+      unsigned v;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ob + (unsigned)(o & 255)) : "memory");
+      *reinterpret_cast<unsigned*>(ops + o) = v;
+    }
+    flushed = upto;
+  };
+  const int li = lane >> 3, lj = lane & 7;
+  while (i > 0 && j > 0) {
+    const int w = (i - 1) & (kBandRows - 1);
+    const int t = w >> 3;
+    const int b = (i - 1) / kBandRows;
+    {
+      const int tl = t > 0 ? t - 1 : 0;
+      const int s = Y::step(t, w & 7, j, Y::hb(b));
+      if (b != tb || s < C::TS * tq || tl < tt0 || t >= tt0 + C::TL) {
+        const int q = s / C::TS;
+        drain();
+        flush(Lc & ~3);
+        const int nt0 = max(0, t - (C::TL - 3));
+        issue(b, q, nt0);
+        drain();
+        tb = b; tq = q; tt0 = nt0;
+      }
+    }
+    // this lane's cell (ci, cj) = (i - li, j - lj)
+    const int ci = i - li, cj = j - lj;
+    unsigned code = 0;
+    if (ci >= 1 && cj >= 1) {
+      const int ww = ci - 1 - tb * kBandRows;
+      const int hh = Y::hb(tb);
+      const int tt = ww >> 3, rr = ww & 7, ss = Y::step(tt, rr, cj, hh);
+      const int slo = C::TS * tq - C::OV * SPC, shi = C::TS * tq + C::TS;
+      const int cbase = C::TC * tq - C::OV;
+      if (ww >= 0 && tt >= tt0 && tt < tt0 + C::TL && ss >= slo && ss < shi) {
+        const unsigned ad = lds_addr(&L.tile[0][0]) + 4u * (unsigned)(((ss / SPC - cbase) * RPC + rr) * C::TL + (tt - tt0));
+        unsigned v;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ad) : "memory");
+        code = (v >> Y::shift(ss, rr, hh)) & 15u;
+      } else {
+        code = getG_global<4, 2>(a.mat, pd, bdw, ci, cj);
+      }
+    }
+    // scalar walk through the block
+    int di = 0, dj = 0;
+    for (;;) {
+      const unsigned c = __builtin_amdgcn_readlane(code, di * 8 + dj);
+      unsigned op = 0;
+      if (st == 0) {
+        const unsigned src = c & 3u;
+        if (src == 0) {
+          op = 'D';
+          ++di; ++dj;
+        } else if (src == 1) {
+          st = 1;  // the gap step below runs from this same cell
+        } else if (src == 3) {
+          st = 2;
+        } else {
+          bad = true;  // not a code the fill writes
+          break;
+        }
+      }
+      if (st == 1) {
+        const bool ext = (c >> 2) & 1u;
+        op = ext ? 'U' : 'u';
+        st = ext ? 1u : 0u;
+        ++di;
+      } else if (st == 2) {
+        const bool ext = (c >> 3) & 1u;
+        op = ext ? 'L' : 'l';
+        st = ext ? 2u : 0u;
+        ++dj;
+      }
+      asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(op) : "memory");
+      ++Lc;
+      if (di > 7 || dj > 7 || i - di <= 0 || j - dj <= 0) break;
+    }
+    i -= di;
+    j -= dj;
+    if (Lc - flushed >= 160) flush(Lc & ~3);
+    if (bad || Lc > pd.m + pd.n) {
+      if (lane == 0) atomicOr(a.err, 16u);
+      break;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  flush(Lc);
+  drain();
+  if (lane == 0) {
+    a.oplen[pd.slot] = Lc;
+    a.endij[pd.slot] = make_int2(i, j);
+  }
+}
+
+__global__ __launch_bounds__(256) void nw_align_pka(FillArgs a) {
+  constexpr int W = 4;
+  __shared__ __attribute__((aligned(16))) int ringH_all[4][128];
+  __shared__ __attribute__((aligned(16))) int ringF_all[4][128];
+  // SEL64 window per super-block: SEL64[64sb-64 .. 64sb+64), two slots per wave
+  __shared__ __attribute__((aligned(16))) unsigned swin_all[4][256];
+  __shared__ __attribute__((aligned(16))) TbLds<W, 2> tbl[4];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  int* ringH = ringH_all[wid];
+  int* ringF = ringF_all[wid];
+  unsigned* swin = swin_all[wid];
+  const unsigned upsel = lane == 0 ? 0x05040100u : 0x07060504u;
+  const int go = a.go, ge = a.ge;
+  const unsigned goe4 = (unsigned)(4 * (go + ge)) * 0x10001u, ge4 = (unsigned)(4 * ge) * 0x10001u;
+
+  for (;;) {
+    unsigned tk = 0;
+    if (lane == 0) tk = atomicAdd(a.counter, 1u);
+    tk = __builtin_amdgcn_readfirstlane(tk);
+    if (tk >= (unsigned)a.ntasks) return;
+    if (__hip_atomic_load((gu32*)a.err, RLX_AGENT) != 0u) return;
+    const int2 task = a.tasks[tk];
+    const PairDesc pd = a.pairs[task.x];
+    const int bp = task.y;                    // band pair: bands 2bp, 2bp+1
+    const int ntp = (pd.nbands + 1) >> 1;     // band pairs of the pair
+    const int R = 2 * bp * kBandRows;         // rows above band 2bp (0-based first row of the band pair)
+    const int row0 = R + lane * kRows;
+    unsigned pl[kRows], ph[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      unsigned p0 = 0, p1 = 0;
+      const unsigned c0 = row0 + r < pd.m ? a.codes[pd.x_off + row0 + r] : 0u;
+      const unsigned c1 = row0 + kBandRows + r < pd.m ? a.codes[pd.x_off + row0 + kBandRows + r] : 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        p0 |= ((unsigned)(c0 == (unsigned)q ? 0 : 4 * a.K1) & 0xffu) << (8 * q);
+        p1 |= ((unsigned)(c1 == (unsigned)q ? 0 : 4 * a.K1) & 0xffu) << (8 * q);
+      }
+      pl[r] = p0;
+      ph[r] = p1;
+    }
+
+    const bool from_above = bp > 0;
+    const bool to_below = bp + 1 < ntp;
+    const int64_t bstride = (int64_t)pd.nchunks * 64;
+    const int64_t fbase = (int64_t)(ntp - 1) * bstride;  // F rows follow the H rows
+    const u64* ginH = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)(bp > 0 ? bp - 1 : 0) * bstride + lane;
+    const u64* ginF = ginH + fbase;
+    const int last_chunk = pd.nchunks > 0 ? pd.nchunks - 1 : 0;
+    u64* goutH = a.bnd + pd.bnd_off + (int64_t)bp * bstride + lane;
+    u64* goutF = goutH + fbase;
+    unsigned* mptr = a.mat + pd.mat_off + (int64_t)bp * 2 * band_dwords(W, pd.sblocks) + lane;
+
+    // bases: H(first row of the half, column 0) = go + (row + 1) ge, so the
+    // border of lane t's row r is kPkaBias + 4 (8t + r) ge in both halves
+    int base_lo = go + (R + 1) * ge, base_hi = go + (R + kBandRows + 1) * ge;
+    const unsigned hb0 = (unsigned)(kPkaBias + 4 * 8 * lane * ge) * 0x10001u;
+    unsigned Hc[kRows], Ec[kRows], Nb[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      Hc[r] = hb0 + (unsigned)r * ge4;
+      Ec[r] = (unsigned)(kPkaInf | 3) * 0x10001u;
+      Nb[r] = 0;
+    }
+    // diag of lane 0's first cell: H(R, 0) (= 0 above the first row)
+    unsigned U = (unsigned)(kPkaBias + 4 * (8 * lane - 1) * ge) * 0x10001u;
+    if (lane == 0 && bp == 0) U = (U & 0xffff0000u) | (unsigned)(kPkaBias - 4 * (go + ge));
+    unsigned F7 = (unsigned)(kPkaInf | 1) * 0x10001u, stH = 0, stF = 0;
+    u64 pH = 0, pF = 0;
+    const unsigned* Sg = a.sel + pd.e_off - 64 + lane;
+    unsigned sw0, sw1;
+    asm_load_S2(Sg, sw0, sw1);
+    asm_load_granule(ginH, pH);
+    asm_load_granule(ginF, pF);
+    wait_vm_keep4<0>(sw0, sw1, pH, pF);
+    bool ok = true;
+    constexpr int kBlockStores = 2 * kRows;
+
+    for (int sb = 0; sb < pd.sblocks; ++sb) {
+      // --- band-above H and F rows for this super-block's columns 64sb+1 .. 64sb+64
+      int bh = go + (64 * sb + lane + 1) * ge, bf = 0;  // band pair 0: H[0][j]; F[0][j] = +inf
+      if (from_above) {
+        bh = 0;
+        if (sb < pd.nchunks) {
+          if (!__all((unsigned)(pH >> 32) == a.epoch)) pH = wait_granules(ginH + 64 * sb, a.epoch, pH, a.err);
+          if (!__all((unsigned)(pF >> 32) == a.epoch)) pF = wait_granules(ginF + 64 * sb, a.epoch, pF, a.err);
+          if (!__all((unsigned)(pH >> 32) == a.epoch && (unsigned)(pF >> 32) == a.epoch)) { ok = false; break; }
+          bh = (int)(unsigned)pH;
+          bf = (int)(unsigned)pF;
+        }
+      }
+      asm_load_granule(ginH + 64 * min(sb + 1, last_chunk), pH);
+      asm_load_granule(ginF + 64 * min(sb + 1, last_chunk), pF);
+      // --- re-centre each half's base (after the masked super-blocks 0 and 1)
+      if (sb >= 2) {
+        const unsigned ref = (unsigned)__builtin_amdgcn_readlane((int)Hc[0], 32);
+        const int dlo = (int)(ref & 0xffffu) - kPkaBias, dhi = (int)(ref >> 16) - kPkaBias;  // multiples of 4
+        const unsigned dd = ((unsigned)dlo & 0xffffu) | ((unsigned)dhi << 16);
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+          Hc[r] = pk_sub(Hc[r], dd);
+          Ec[r] = pk_sub(Ec[r], dd);
+        }
+        U = pk_sub(U, dd);
+        F7 = pk_sub(F7, dd);
+        stH = pk_sub(stH, dd);
+        stF = pk_sub(stF, dd);
+        base_lo += dlo / 4;
+        base_hi += dhi / 4;
+      }
+      int* slH = ringH + (sb & 1) * 64;
+      int* slF = ringF + (sb & 1) * 64;
+      // past the last chunk (columns > n, read by nothing that is kept) the up
+      // row is the base itself: every half stays inside [0, 32767] for the
+      // carry-free v_add_u32, junk columns included
+      const bool real_up = !from_above || sb < pd.nchunks;
+      slH[lane] = real_up ? (int)((unsigned)(4 * (bh - base_lo) + kPkaBias) & 0xffffu) : kPkaBias;
+      slF[lane] = from_above && sb < pd.nchunks ? (int)(((unsigned)(4 * (bf - base_lo) + kPkaBias) | 1u) & 0xffffu)
+                                                : (kPkaInf | 1);
+      unsigned* w = swin + (sb & 1) * 128;
+      w[lane] = sw0;
+      w[64 + lane] = sw1;
+      asm_load_S2(Sg + 64 * (sb + 1), sw0, sw1);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+
+      const bool pub_sb = to_below && sb >= 2 && sb - 2 < pd.nchunks;
+      u64* gpH = goutH + 64 * (sb >= 2 ? sb - 2 : 0);
+      u64* gpF = goutF + 64 * (sb >= 2 ? sb - 2 : 0);
+      for (int blk = 0; blk < 8; ++blk) {
+        const int s0 = sb * 64 + blk * 8;
+        const unsigned* srow = w + blk * 8 + 64 - lane;
+        const bool pub = pub_sb && blk == 7;
+        if (sb < 2)
+          step_block_pka<true>(s0, lane, Hc, Ec, Nb, F7, U, stH, stF, pl, ph, srow, slH + blk * 8, slF + blk * 8, upsel,
+                               mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0);
+        else
+          step_block_pka<false>(s0, lane, Hc, Ec, Nb, F7, U, stH, stF, pl, ph, srow, slH + blk * 8, slF + blk * 8,
+                                upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0);
+        mptr += 2 * kRows * kWave;
+        wait_vm_keep4<kBlockStores>(sw0, sw1, pH, pF);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (!ok) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add((gu32*)(a.done + pd.slot), 1u, RLX_AGENT);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    // the pair's last band pair: every task has released, so acquire and trace here
+    if (prev + 1u == (unsigned)ntp) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (a.dbg_notrace) {
+        if (lane == 0) { a.oplen[pd.slot] = 0; a.endij[pd.slot] = make_int2(pd.m, pd.n); }
+      } else {
+        trace_pair_pka(a, pd, tbl[wid], lane);
+      }
+    }
+  }
+}
+
+// ===========================================================================
 // Profile-profile fill of the progressive SoP MSA (oracle
 // msa_oracle.c nwo_profile_align):
 //   H = min(H[i-1][j-1] + sub(i,j), H[i-1][j] + gx(i), H[i][j-1] + gy(j))
@@ -1925,6 +2334,10 @@ hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStrea
       if (bits != 4) return hipErrorInvalidValue;
       hipLaunchKernelGGL(nw_profile, dim3(grid), dim3(256), 0, s, a);
       return hipGetLastError();
+    case kAffinePk:
+      if (bits != 4) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(nw_align_pka, dim3(grid), dim3(256), 0, s, a);
+      return hipGetLastError();
     case kProfile: return fill_m<kProfile>(bits, a, grid, s);
     case kCompare: return fill_m<kCompare>(bits, a, grid, s);
     case kLiteral: return bits == 32 ? fill_w<kLiteral, 32>(a, grid, s) : hipErrorInvalidValue;
@@ -1942,9 +2355,10 @@ static int occ_w() {
 
 int fill_blocks_per_cu(int mode, int bits) {
   if (mode == kLiteral) return occ_w<kLiteral, 32>();
-  if (mode == kAffine || mode == kPacked || mode == kPacked2 || mode == kProfileDP) {
+  if (mode == kAffine || mode == kPacked || mode == kPacked2 || mode == kProfileDP || mode == kAffinePk) {
     int n = 0;
     const void* f = mode == kAffine     ? reinterpret_cast<const void*>(&nw_align_affine)
+                    : mode == kAffinePk ? reinterpret_cast<const void*>(&nw_align_pka)
                     : mode == kPacked   ? reinterpret_cast<const void*>(&nw_align_pk)
                     : mode == kPacked2  ? reinterpret_cast<const void*>(&nw_align_pk2)
                                         : reinterpret_cast<const void*>(&nw_profile);

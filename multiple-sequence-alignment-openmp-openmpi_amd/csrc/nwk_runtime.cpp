@@ -352,12 +352,29 @@ struct Scoring {
   int go, ge;
 };
 
+// nw_align_pka keeps H, E and F as 4 x (value - base) + tag + kPkaBias in int16
+// halves.  H is (go + ge)-Lipschitz in the Manhattan distance (one gap step
+// changes it by at most go + ge); a half's cells at one step lie
+// within distance 640 of its base cell, re-centred every 64 steps, and E, F, the
+// diagonal candidate sit at most 2(go + ge) + pxy above H.  So every value stays
+// inside [0, 32000) when 4 (650 (go + ge) + pxy + 4) <= 15900 (bias 16000,
+// +inf 32000, kernels:"Packed affine fill").  The profile bytes hold 4 pxy.
+bool pka_admissible(const Scoring& sc) {
+  if (sc.pxy < 0 || sc.go < 0 || sc.ge < 0 || 4 * (int64_t)sc.pxy > 255) return false;
+  return 4 * (650 * ((int64_t)sc.go + sc.ge) + sc.pxy + 4) <= 15900;
+}
+
 int choose_plan(const nwk_ctx* c, const Scoring& sc, Plan* pl) {
   const int pxy = sc.pxy, pgap = sc.pgap;
   if (sc.affine) {
-    pl->mode = kAffine;
-    pl->bits = 4;  // 4-bit traceback codes
-    pl->kind = 1;  // raw bytes (compare)
+    // packed band pairs (nw_align_pka) where the int16 window provably holds
+    // and the alphabet fits the 4-entry profile; opts.kernel = 1 (unpacked) or
+    // NWK_AFFPK=0 keeps nw_align_affine
+    static const int affpk_env = getenv("NWK_AFFPK") ? atoi(getenv("NWK_AFFPK")) : 1;
+    const bool pk = c->opts.kernel != 1 && affpk_env != 0 && c->alpha <= 4 && pka_admissible(sc);
+    pl->mode = pk ? kAffinePk : kAffine;
+    pl->bits = 4;          // 4-bit traceback codes
+    pl->kind = pk ? 0 : 1;  // profile codes / raw bytes (compare)
     pl->K0 = 0;
     pl->K1 = pxy;
     return NWK_OK;
@@ -390,9 +407,10 @@ int choose_plan(const nwk_ctx* c, const Scoring& sc, Plan* pl) {
 
 // 64-step super-blocks per band: the last band-row value of column n leaves
 // lane 63 at step n + 62 (nw_align) or n + 126 (nw_align_pk, 2-column skew).
-inline int sblocks_of(int mode, int64_t nch) { return (int)(nch + (mode == kPacked || mode == kPacked2 ? 2 : 1)); }
-// Fill tasks per pair: bands, or band pairs (kPacked2).
-inline int64_t tasks_of(int mode, int64_t nb) { return mode == kPacked2 ? (nb + 1) / 2 : nb; }
+inline bool band_pairs(int mode) { return mode == kPacked2 || mode == kAffinePk; }
+inline int sblocks_of(int mode, int64_t nch) { return (int)(nch + (mode == kPacked || band_pairs(mode) ? 2 : 1)); }
+// Fill tasks per pair: bands, or band pairs (kPacked2, kAffinePk).
+inline int64_t tasks_of(int mode, int64_t nb) { return band_pairs(mode) ? (nb + 1) / 2 : nb; }
 
 // kPacked2 segmented traceback footprint for a speculative segment every E
 // tasks (E = 0: one whole-pair segment): move buffers (segment k starts on
@@ -420,7 +438,7 @@ void footprint(PairWork* w, int bits, int mode, bool affine) {
   w->segops_b = w->segctl_b = 0;
   w->spec = 0;
   if (segmented(mode)) seg_footprint(w, mode, 0, 1);
-  w->mat_dw = (mode == kPacked2 ? 2 * nt : nb) * band_dwords(bits, sblocks_of(mode, nch));
+  w->mat_dw = (band_pairs(mode) ? 2 * nt : nb) * band_dwords(bits, sblocks_of(mode, nch));
   w->bnd_gr = (nt - 1) * nch * 64 * (affine ? 2 : 1);  // affine: H and F boundary rows
   w->ops_b = round_up((int64_t)w->m + w->n, 16);
 }
@@ -769,8 +787,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   }
   if (!dp.empty()) {
     if ((rc = build_encoding(c, pl.kind)) != NWK_OK) return rc;
-    if ((pl.mode == kPacked || pl.mode == kPacked2) &&
-        (rc = build_sel(c, pl.K0 < 0 ? 1 : 0, pl.mode == kPacked2 ? 64 : 1)) != NWK_OK)
+    if ((pl.mode == kPacked || band_pairs(pl.mode)) &&
+        (rc = build_sel(c, pl.K0 < 0 ? 1 : 0, band_pairs(pl.mode) ? 64 : 1)) != NWK_OK)
       return rc;
   }
   // Largest first (LPT inside the device; longest bands dequeued first).
@@ -816,6 +834,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   // nw_align_affine: 2 waves/SIMD beat 3 by ~4% kernel GCUPS on big13 and C5
   // (profiles/r01/ab_affine_bpc.json)
   if (pl.mode == kAffine) bpc = std::min(bpc, 2);
+  if (pl.mode == kAffinePk) bpc = std::min(bpc, 2);
   static const int bpc_cap = getenv("NWK_BPC") ? atoi(getenv("NWK_BPC")) : 0;
   if (bpc_cap > 0) bpc = std::min(bpc_cap, fill_blocks_per_cu(pl.mode, pl.bits));
   const int grid = bpc * c->cus;
@@ -1012,7 +1031,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.codes = c->d_codes[pl.kind].as<uint8_t>();
     fa.E = c->d_E[pl.kind].as<uint32_t>();
     fa.sel = pl.mode == kPacked    ? c->d_sel[pl.K0 < 0 ? 1 : 0].as<uint32_t>()
-             : pl.mode == kPacked2 ? c->d_sel[2 + (pl.K0 < 0 ? 1 : 0)].as<uint32_t>()
+             : band_pairs(pl.mode) ? c->d_sel[2 + (pl.K0 < 0 ? 1 : 0)].as<uint32_t>()
                                    : nullptr;
     fa.mat = c->d_work.as<uint32_t>();
     fa.bnd = c->d_work.as<unsigned long long>();

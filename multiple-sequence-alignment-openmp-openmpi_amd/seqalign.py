@@ -23,9 +23,11 @@ LIB_PATH = os.path.join(HERE, "lib", "libnwk.so")
 
 NWK_OK = 0
 ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "EKERNEL", -5: "ECOMM"}
-MODES = {0: "profile", 1: "compare", 2: "literal", 3: "affine", 4: "packed-profile", 5: "packed-band-pairs"}
+MODES = {0: "profile", 1: "compare", 2: "literal", 3: "affine", 4: "packed-profile", 5: "packed-band-pairs",
+         7: "packed-affine-band-pairs"}
 # fill kernel of each mode (csrc/nwk_kernels.hip), as rocprofv3 names it
-KERNELS = {0: "nw_align", 1: "nw_align", 2: "nw_align", 3: "nw_align_affine", 4: "nw_align_pk", 5: "nw_align_pk2"}
+KERNELS = {0: "nw_align", 1: "nw_align", 2: "nw_align", 3: "nw_align_affine", 4: "nw_align_pk", 5: "nw_align_pk2",
+           7: "nw_align_pka"}
 
 
 class NwkError(RuntimeError):

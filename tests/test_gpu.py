@@ -216,6 +216,69 @@ def test_affine_random_vs_oracle(engine, pxy, go, ge):
     assert seqalign.chain_hash(hs) == h
 
 
+# Packed affine fill (nw_align_pka, mode 7): ACGT-only sets with admissible
+# penalties run on it by default; every result must equal the oracle and the
+# unpacked nw_align_affine (opts.kernel = "nw_align" forces the latter).
+PKA_PARAMS = [(3, 3, 1), (1, 2, 2), (0, 5, 0), (7, 0, 3), (2, 1, 1), (5, 0, 0), (0, 0, 0), (9, 3, 2), (6, 6, 0)]
+PKA_LENS = [1, 2, 63, 64, 65, 511, 512, 513, 1023, 1024, 1025, 2100]
+
+
+@pytest.mark.parametrize("pxy,go,ge", PKA_PARAMS)
+def test_affine_packed_vs_oracle(engine, pxy, go, ge):
+    r = random.Random(7000 + pxy * 100 + go * 10 + ge)
+    genes = [bytes(r.choice(ACGT) for _ in range(L)) for L in PKA_LENS]
+    genes += _mutants(r, bytes(r.choice(ACGT) for _ in range(1500)), 3, ACGT)
+    engine.set_sequences(genes)
+    pen, hs = engine.align_pairs_affine(_all_ids(len(genes)), pxy, go, ge)
+    assert engine.stats()["mode"] == 7, "nw_align_pka expected"
+    h, opens, ohs = oracle.all_pairs_affine(genes, pxy, go, ge)
+    assert [int(v) for v in pen] == opens
+    assert [x.tobytes().hex() for x in hs] == ohs
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_affine_packed_equals_unpacked(seed):
+    """Multi-band-pair pairs (3k-7k): nw_align_pka vs nw_align_affine, bit-exact."""
+    r = random.Random(8100 + seed)
+    base = bytes(r.choice(ACGT) for _ in range(5000))
+    genes = _rand_genes(r, 3, 3000, 7000, ACGT) + _mutants(r, base, 3, ACGT) + [b"A" * 4000, b"C" * 2500]
+    pxy, go, ge = [(3, 3, 1), (4, 2, 1), (2, 4, 2)][seed]
+    out = []
+    for kernel in ("auto", "nw_align"):
+        with seqalign.Engine(device=0, kernel=kernel) as e:
+            e.set_sequences(genes)
+            h, pen, hs = e.align_all(pxy, None, affine=(go, ge))
+            out.append((e.stats()["mode"], h, [int(v) for v in pen], hs.tobytes()))
+    assert out[0][0] == 7 and out[1][0] == 3
+    assert out[0][1:] == out[1][1:]
+
+
+def test_affine_packed_big13_degenerate(engine, golden):
+    """big13 at full size on nw_align_pka with go=0, ge=pgap: the reference's published answer."""
+    c = golden["big13"]
+    pxy, pgap, genes = case_input(c)
+    engine.set_sequences(genes)
+    pen, hs = engine.align_pairs_affine(_all_ids(len(genes)), pxy, 0, pgap)
+    assert engine.stats()["mode"] == 7
+    assert [int(v) for v in pen] == c["penalties"]
+    assert seqalign.chain_hash(hs) == c["hash"]
+
+
+def test_affine_packed_not_used_where_inadmissible(engine):
+    """go + ge too large for the int16 window, or > 4 symbols: nw_align_affine runs."""
+    r = random.Random(91)
+    genes = _rand_genes(r, 4, 100, 900, ACGT)
+    engine.set_sequences(genes)
+    pen, _ = engine.align_pairs_affine(_all_ids(4), 4, 10, 1)
+    assert engine.stats()["mode"] == 3
+    assert [int(v) for v in pen] == oracle.all_pairs_affine(genes, 4, 10, 1)[1]
+    genes5 = genes + [b"ACGTN" * 50]
+    engine.set_sequences(genes5)
+    pen, _ = engine.align_pairs_affine(_all_ids(5), 3, 3, 1)
+    assert engine.stats()["mode"] == 3
+    assert [int(v) for v in pen] == oracle.all_pairs_affine(genes5, 3, 3, 1)[1]
+
+
 @pytest.mark.parametrize("m,n", [(1, 1), (1, 9), (9, 1), (700, 30), (30, 700), (1100, 1030), (2000, 64)])
 def test_affine_single_pair_strings(engine, m, n):
     r = random.Random(m * 7 + n)
