@@ -1784,7 +1784,7 @@ __device__ __forceinline__ void step_block_pka(int s0, int lane, unsigned (&Hc)[
                                                unsigned& stF, const unsigned (&pl)[kRows], const unsigned (&ph)[kRows],
                                                const unsigned* srow, const int* bH, const int* bF, unsigned upsel,
                                                unsigned* mptr, bool pub, u64* gpH, u64* gpF, unsigned epoch,
-                                               int base_hi, unsigned goe4, unsigned ge4, unsigned hb0) {
+                                               int base_hi, unsigned goe4, unsigned ge4, unsigned hb0, unsigned xfer) {
   const int4 hA = *reinterpret_cast<const int4*>(bH), hB = *reinterpret_cast<const int4*>(bH + 4);
   const int4 fA = *reinterpret_cast<const int4*>(bF), fB = *reinterpret_cast<const int4*>(bF + 4);
   const int bh[8] = {hA.x, hA.y, hA.z, hA.w, hB.x, hB.y, hB.z, hB.w};
@@ -1805,8 +1805,9 @@ __device__ __forceinline__ void step_block_pka(int s0, int lane, unsigned (&Hc)[
     // row 0's up: lane t-1's row 7 (previous step); lane 0: {band above, lane 63's band-2p row 7}
     const unsigned xH = (unsigned)__builtin_amdgcn_update_dpp(0, (int)Hc[kRows - 1], 0x13c /*wave_ror:1*/, 0xf, 0xf, false);
     const unsigned xF = (unsigned)__builtin_amdgcn_update_dpp(0, (int)F7, 0x13c, 0xf, 0xf, false);
-    unsigned hup = __builtin_amdgcn_perm(xH, (unsigned)bh[k], upsel);
-    unsigned fup = __builtin_amdgcn_perm(xF, (unsigned)bf[k], upsel);
+    // lane 0's high half takes lane 63's low-half row: rebase it from base_lo to base_hi (xfer)
+    unsigned hup = __builtin_amdgcn_perm(xH, (unsigned)bh[k], upsel) + xfer;
+    unsigned fup = __builtin_amdgcn_perm(xF, (unsigned)bf[k], upsel) + xfer;
     unsigned hdg = U;
     U = hup;
     unsigned sk = sel[k];
@@ -1867,7 +1868,8 @@ __device__ __forceinline__ void step_block_pka(int s0, int lane, unsigned (&Hc)[
 // Traceback of one pair on nw_align_pka's codes (layout LY 2), the same LDS
 // tile staging as trace_pair and the three-state walk of trace_pair_affine:
 // 'D', 'U'/'L' (gap extended) and 'u'/'l' (the gap's first column).
-__device__ __forceinline__ void trace_pair_pka(const FillArgs& a, const PairDesc& pd, TbLds<4, 2>& L, int lane) {
+__device__ __forceinline__ void trace_pair_pka(const FillArgs& a, const PairDesc& pd, TbLds<4, 2>& L, int lane,
+                                               unsigned* prog) {
   using C = TbConf<4, 2>;
   using Y = Lay<4, 2>;
   constexpr int SPC = Y::SPC, RPC = Y::RPC;
@@ -1902,6 +1904,9 @@ __device__ __forceinline__ void trace_pair_pka(const FillArgs& a, const PairDesc
   };
   const int li = lane >> 3, lj = lane & 7;
   while (i > 0 && j > 0) {
+    if (prog && lane == 0)
+      __hip_atomic_store((gu32*)prog, 0x50000000u | ((unsigned)(Lc & 0xff) << 20) | ((unsigned)(i & 0x3ff) << 10) | (unsigned)(j & 0x3ff),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const int w = (i - 1) & (kBandRows - 1);
     const int t = w >> 3;
     const int b = (i - 1) / kBandRows;
@@ -2002,12 +2007,14 @@ __global__ __launch_bounds__(256) void nw_align_pka(FillArgs a) {
   const unsigned upsel = lane == 0 ? 0x05040100u : 0x07060504u;
   const int go = a.go, ge = a.ge;
   const unsigned goe4 = (unsigned)(4 * (go + ge)) * 0x10001u, ge4 = (unsigned)(4 * ge) * 0x10001u;
+  unsigned* prog = a.prog ? a.prog + blockIdx.x * 4 + wid : nullptr;  // NWK_WATCHDOG progress markers
 
   for (;;) {
     unsigned tk = 0;
     if (lane == 0) tk = atomicAdd(a.counter, 1u);
     tk = __builtin_amdgcn_readfirstlane(tk);
-    if (tk >= (unsigned)a.ntasks) return;
+    PROG(0x10000000u | tk);
+    if (tk >= (unsigned)a.ntasks) { PROG(0x60000000u); return; }
     if (__hip_atomic_load((gu32*)a.err, RLX_AGENT) != 0u) return;
     const int2 task = a.tasks[tk];
     const PairDesc pd = a.pairs[task.x];
@@ -2067,6 +2074,7 @@ __global__ __launch_bounds__(256) void nw_align_pka(FillArgs a) {
     constexpr int kBlockStores = 2 * kRows;
 
     for (int sb = 0; sb < pd.sblocks; ++sb) {
+      PROG(0x20000000u | (unsigned)sb);
       // --- band-above H and F rows for this super-block's columns 64sb+1 .. 64sb+64
       int bh = go + (64 * sb + lane + 1) * ge, bf = 0;  // band pair 0: H[0][j]; F[0][j] = +inf
       if (from_above) {
@@ -2115,6 +2123,8 @@ __global__ __launch_bounds__(256) void nw_align_pka(FillArgs a) {
       __builtin_amdgcn_wave_barrier();
 
       const bool pub_sb = to_below && sb >= 2 && sb - 2 < pd.nchunks;
+      // scaled base_lo - base_hi in lane 0's high half (multiple of 4: tags kept)
+      const unsigned xfer = lane == 0 ? (unsigned)(4 * (base_lo - base_hi)) << 16 : 0u;
       u64* gpH = goutH + 64 * (sb >= 2 ? sb - 2 : 0);
       u64* gpF = goutF + 64 * (sb >= 2 ? sb - 2 : 0);
       for (int blk = 0; blk < 8; ++blk) {
@@ -2123,15 +2133,16 @@ __global__ __launch_bounds__(256) void nw_align_pka(FillArgs a) {
         const bool pub = pub_sb && blk == 7;
         if (sb < 2)
           step_block_pka<true>(s0, lane, Hc, Ec, Nb, F7, U, stH, stF, pl, ph, srow, slH + blk * 8, slF + blk * 8, upsel,
-                               mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0);
+                               mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0, xfer);
         else
           step_block_pka<false>(s0, lane, Hc, Ec, Nb, F7, U, stH, stF, pl, ph, srow, slH + blk * 8, slF + blk * 8,
-                                upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0);
+                                upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0, xfer);
         mptr += 2 * kRows * kWave;
         wait_vm_keep4<kBlockStores>(sw0, sw1, pH, pF);
       }
       __builtin_amdgcn_wave_barrier();
     }
+    PROG(0x30000000u);
     if (!ok) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -2146,7 +2157,9 @@ __global__ __launch_bounds__(256) void nw_align_pka(FillArgs a) {
       if (a.dbg_notrace) {
         if (lane == 0) { a.oplen[pd.slot] = 0; a.endij[pd.slot] = make_int2(pd.m, pd.n); }
       } else {
-        trace_pair_pka(a, pd, tbl[wid], lane);
+        PROG(0x40000000u);
+        trace_pair_pka(a, pd, tbl[wid], lane, prog);
+        PROG(0x56000000u);
       }
     }
   }

@@ -81,6 +81,16 @@ struct DevBuf {
     cap = 0;
     HIP_TRY(hipMalloc(&p, bytes));
     cap = bytes;
+    // debug: NWK_POISON=<byte> fills fresh device buffers, so a read of memory no
+    // kernel or copy has written shows up as a wrong answer on every run
+    // (buffers of at least NWK_POISON_MIN bytes; the fill completes before the
+    // engine's own stream uses the buffer)
+    static const int poison = getenv("NWK_POISON") ? atoi(getenv("NWK_POISON")) : -1;
+    static const long long poison_min = getenv("NWK_POISON_MIN") ? atoll(getenv("NWK_POISON_MIN")) : 0;
+    if (poison >= 0 && (long long)bytes >= poison_min) {
+      HIP_TRY(hipMemset(p, poison & 0xff, bytes));
+      HIP_TRY(hipDeviceSynchronize());
+    }
     return NWK_OK;
   }
   void release() {

@@ -288,14 +288,16 @@ def test_affine_single_pair_strings(engine, m, n):
         assert engine.get_minimum_penalty_affine(x, y, pxy, go, ge) == oracle.pair_affine(x, y, pxy, go, ge)
 
 
-def test_affine_multi_batch_and_api(golden):
+@pytest.mark.parametrize("kernel,mode", [("auto", 7), ("nw_align", 3)])
+def test_affine_multi_batch_and_api(golden, kernel, mode):
+    """Multi-batch workspaces on nw_align_pka (default for ACGT) and nw_align_affine."""
     r = random.Random(21)
     genes = _rand_genes(r, 7, 600, 1300, ACGT)
-    with seqalign.Engine(device=0, workspace_bytes=3 << 20) as e:
+    with seqalign.Engine(device=0, workspace_bytes=3 << 20, kernel=kernel) as e:
         e.set_sequences(genes)
         pen, hs = e.align_pairs_affine(_all_ids(len(genes)), 3, 4, 1)
         st = e.stats()
-        assert st["batches"] > 1 and st["mode"] == 3
+        assert st["batches"] > 1 and st["mode"] == mode
     h, opens, ohs = oracle.all_pairs_affine(genes, 3, 4, 1)
     assert [int(v) for v in pen] == opens and [x.tobytes().hex() for x in hs] == ohs
     pens = [0] * len(opens)

@@ -30,7 +30,7 @@ for s in $STEPS; do
         ls /opt/conda/bin/mpirun 2>&1; echo "OMP_NUM_THREADS=${OMP_NUM_THREADS:-}"; rocm-smi --showuse 2>&1 | head -20; } > "$OUT/host.txt" 2>&1
       ;;
     tests)
-      run pytest_gpu 1000 python -u -m pytest tests/ -x -v -m gpu --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
+      run pytest_gpu 1000 python -u -m pytest tests/ -x -v -m gpu --timeout 150 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
       ;;
     bench)
       run bench_$WL 600 python3 bench.py --workload "$WL" --steps "${BSTEPS:-5}" --warmup 1 $BENCH_ARGS
