@@ -72,6 +72,23 @@ __device__ __forceinline__ void wait_vm_keep(unsigned& a, unsigned& b, u64& c) {
   asm volatile("s_waitcnt vmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "n"(N) : "memory");
 }
 
+// The same, but waits for every outstanding op when `all` (wave-uniform) is
+// set -- one asm block, so the compiler never copies a register between two
+// differently counted waits (a copy made before the wait reads the old value).
+template <int N>
+__device__ __forceinline__ void wait_vm_keep_or_all(bool all, unsigned& a, unsigned& b, u64& c) {
+  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+  asm volatile(
+      "s_cmp_eq_u32 %[all], 0\n\t"
+      "s_cbranch_scc1 .Lnwk_keep%=\n\t"
+      "s_waitcnt vmcnt(0)\n"
+      ".Lnwk_keep%=:\n\t"
+      "s_waitcnt vmcnt(%[n])"
+      : "+v"(a), "+v"(b), "+v"(c)
+      : [all] "s"(__builtin_amdgcn_readfirstlane(all ? 1 : 0)), [n] "n"(N)
+      : "memory", "scc");
+}
+
 // A zero the optimiser cannot see: LLVM rewrites an idempotent atomic RMW
 // (add 0) into a plain atomic load, which can be served by a stale copy in
 // this XCD's L2.  A real RMW is performed at the coherence point.
@@ -724,8 +741,9 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
         mptr += (8 / SPD) * kRows * kWave;
         // the window / granule prefetches are older than this block's
         // kBlockStores stores: waiting for the rest leaves those in flight
-        // (a no-op after block 0)
-        wait_vm_keep<kBlockStores>(ew0, ew1, pend);
+        // (a no-op after block 0).  The linear-space fill pass stores nothing,
+        // so there the count would not cover the prefetches: wait for all.
+        wait_vm_keep_or_all<kBlockStores>(!store, ew0, ew1, pend);
       }
       // --- publish chunk sb (columns 64sb-63 .. 64sb of our last row) for band+1
       if (to_below && sb >= 1 && sb <= pd.nchunks) st_granule(gout + 64 * (sb - 1), a.epoch, stage);

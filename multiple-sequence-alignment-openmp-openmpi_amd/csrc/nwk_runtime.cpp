@@ -218,6 +218,7 @@ int nwk_ctx_create(const nwk_opts* opts, nwk_ctx** out) {
   nwk_opts o;
   nwk_opts_default(&o);
   if (opts) o = *opts;
+  if (const char* v = getenv("NWK_VERBOSE")) o.verbose = atoi(v);  // debug: diagnostics on stderr
   if (ndev <= 0) return fail(NWK_EDEVICE, "nwk_ctx_create: no HIP device visible");
   if (o.device < 0 || o.device >= ndev) return fail(NWK_EINVAL, "nwk_ctx_create: device %d of %d", o.device, ndev);
   if (o.finalize < 0 || o.finalize > 2) return fail(NWK_EINVAL, "nwk_ctx_create: finalize must be 0/1/2");
@@ -637,6 +638,9 @@ int align_linear_batch(nwk_ctx* c, const Plan& pl0, const Scoring& sc, const Pai
   void* const old_work = c->d_work.p;
   if ((rc = c->d_work.ensure((size_t)work_b)) != NWK_OK) return rc;
   if (c->d_work.p != old_work) c->clean_b = 0;
+  static const int lin_zero = getenv("NWK_LIN_ZERO") ? atoi(getenv("NWK_LIN_ZERO")) : 0;  // debug A/B
+  if (lin_zero == 1) c->clean_b = 0;
+  if (lin_zero == 2) HIP_TRY(hipMemsetAsync(c->d_work.p, 0, (size_t)work_b, c->stream));
   if (bnd_need_b > c->clean_b)
     HIP_TRY(hipMemsetAsync(c->d_work.as<uint8_t>() + c->clean_b, 0, (size_t)(bnd_need_b - c->clean_b), c->stream));
   c->clean_b = bnd_need_b;
@@ -646,6 +650,12 @@ int align_linear_batch(nwk_ctx* c, const Plan& pl0, const Scoring& sc, const Pai
   if ((rc = c->d_endij.ensure(sizeof(int2) * np)) != NWK_OK) return rc;
   if ((rc = c->d_done.ensure(sizeof(unsigned) * np)) != NWK_OK) return rc;
   for (int q = 0; q < np; ++q) pd[q].mat_off = scratch_b0 / 4 + scr_off[q];
+  if (c->opts.verbose >= 3) {
+    fprintf(stderr, "nwk linear batch: %d pairs, G %d, budget %lld, work %lld B at %p, clean %lld; ids", np, G,
+            (long long)c->budget, (long long)work_b, c->d_work.p, (long long)c->clean_b);
+    for (int q = 0; q < np; ++q) fprintf(stderr, " %lld", (long long)ws[q].id);
+    fprintf(stderr, "\n");
+  }
   FillArgs fa;
   memset(&fa, 0, sizeof fa);
   fa.pairs = c->d_pairs.as<PairDesc>();

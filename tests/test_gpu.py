@@ -518,14 +518,24 @@ def test_linear_space_when_the_matrix_does_not_fit():
     assert st["linear_space_pairs"] >= 1
 
 
-def test_linear_space_big13(golden):
+def test_linear_space_big13(golden, monkeypatch):
     """Full size (2.785e11 cells) through the linear-space path: the reference's published hash."""
     c = golden["big13"]
     pxy, pgap, genes = case_input(c)
+    monkeypatch.setenv("NWK_VERBOSE", "3")  # batch compositions on stderr (shown on failure)
     with seqalign.Engine(device=0, linear_space=16) as e:
         e.set_sequences(genes)
         pen, hs = e.align_pairs(_all_ids(len(genes)), pxy, pgap)
-    assert [int(v) for v in pen] == c["penalties"]
+        st = e.stats()
+    bad = [q for q in range(len(pen)) if int(pen[q]) != c["penalties"][q]]
+    if bad:  # diagnostics: the failing pairs, the run's batching, and the same pairs again on a fresh engine
+        ij = [seqalign.pair_ij(q) for q in bad]
+        with seqalign.Engine(device=0, linear_space=16) as e2:
+            e2.set_sequences(genes)
+            again, _ = e2.align_pairs(np.array(bad, dtype=np.int64), pxy, pgap)
+        pytest.fail("pairs %s (i, j %s; m x n %s) got %s want %s; stats %s; the same pairs alone: %s" % (
+            bad, ij, [(len(genes[i]), len(genes[j])) for i, j in ij], [int(pen[q]) for q in bad],
+            [c["penalties"][q] for q in bad], st, [int(v) for v in again]))
     assert seqalign.chain_hash(hs) == c["hash"]
 
 

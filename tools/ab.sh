@@ -6,6 +6,6 @@ mkdir -p gpurun_out
 export REPS=${REPS:-4} ROUNDS=${ROUNDS:-2}
 for b in ${BPCS:-2}; do
   echo "== BPC=$b"
-  NWK_BPC=$b timeout -k 10 300 python3 tools/timeit.py "$@" 2>&1 | grep timeit
-  [ -n "${NOTRACE:-}" ] && NWK_NOTRACE=1 NWK_BPC=$b ROUNDS=1 timeout -k 10 120 python3 tools/timeit.py "$1" 2>&1 | grep timeit | sed 's/^/notrace /'
+  NWK_BPC=$b timeout -k 10 300 python3 tools/fill_timeit.py "$@" 2>&1 | grep timeit
+  [ -n "${NOTRACE:-}" ] && NWK_NOTRACE=1 NWK_BPC=$b ROUNDS=1 timeout -k 10 120 python3 tools/fill_timeit.py "$1" 2>&1 | grep timeit | sed 's/^/notrace /'
 done

@@ -3,5 +3,5 @@
 set -euo pipefail
 cd "$(dirname "$0")/.."
 for r in 1 2; do for e in "$@"; do
-  env $e REPS=${REPS:-4} timeout -k 10 120 python3 tools/timeit.py 2>&1 | grep timeit | sed "s/^/[$e] /"
+  env $e REPS=${REPS:-4} timeout -k 10 120 python3 tools/fill_timeit.py 2>&1 | grep timeit | sed "s/^/[$e] /"
 done; done

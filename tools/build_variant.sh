@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Builds a libnwk.so variant with extra compile flags into tools/libvariants/<name>/ (for tools/timeit.py A/B).
+# Builds a libnwk.so variant with extra compile flags into tools/libvariants/<name>/ (for tools/fill_timeit.py A/B).
 # usage: tools/build_variant.sh <name> <flags...>
 set -euo pipefail
 cd "$(dirname "$0")/.."

@@ -1,5 +1,5 @@
 """Times align_pairs on a workload several times in one process (min/median).
-usage: python tools/timeit.py [lib_dir ...]  (each lib dir holds a libnwk.so variant)"""
+usage: python tools/fill_timeit.py [lib_dir ...]  (each lib dir holds a libnwk.so variant)"""
 import sys, os, time, ctypes, importlib
 sys.path.insert(0, "multiple-sequence-alignment-openmp-openmpi_amd")
 import numpy as np

@@ -12,6 +12,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "multiple-sequence-alignment-openmp-openmpi_amd"))
 import numpy as np  # noqa: E402
 
+if os.environ.get("LS_TORCH"):  # load torch's bundled HIP runtime first (as the test session does)
+    import torch  # noqa: F401
 import seqalign  # noqa: E402
 
 G = int(sys.argv[1])
