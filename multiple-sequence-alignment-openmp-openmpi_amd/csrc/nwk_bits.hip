@@ -1,0 +1,435 @@
+// nwk_bits.hip -- bit-sliced anti-diagonal fill (mode kBits, kernel nw_align_bits)
+// for the reference's linear-gap recurrence (skel:211-226, sub:478-487) with
+// pxy >= 0, pgap in {1, 2} and at most four distinct symbols.
+//
+// Difference form.  In G-space (G = H - (i+j) pgap) every
+// cell's vertical and horizontal differences
+//     v(i,j) = G[i-1][j] - G[i][j],   h(i,j) = G[i][j-1] - G[i][j]
+// lie in [0, 2 pgap], and with U = h(i-1,j), L = v(i,j-1)
+//     D = max(S, U, L),  S = 2 pgap (match) or 2 pgap - pxy (mismatch)
+//     v(i,j) = D - U,    h(i,j) = D - L.
+// Borders are all zero.  The reference's traceback (skel:229-262: DIAG on a
+// match, DIAG if H_diag + pxy == H, UP if H_up + pgap == H, else LEFT) needs
+// two bits per cell: diag = match | (D == S_mismatch) and up = (v == 0).
+//
+// Bit slicing.  A value x in [0, NP], NP = 2 pgap, is held as NP thermometer
+// planes t_k = [x > k].  Then max is OR, and D - U is the convolution
+//     t_k(D - U) = OR_j (~t_j(U) & t_{j+k}(D)),
+// so one 32-bit VALU op evaluates one plane term for 32 cells.  Bit b of lane
+// t is row 32 t + b of a 2048-row band; at step s that row is at column
+// s - 32 t - b (one anti-diagonal per step), so a cell's left neighbour is the
+// same bit one step earlier and its upper neighbour is the bit below one step
+// earlier -- a 1-bit funnel shift with lane t-1's top bit (DPP wave_shr:1).
+// Lane 0's bit 0 takes the band above's last row instead: per 64-column chunk
+// that row arrives as 2 NP self-tagged granules {epoch:32 | 32 plane bits}.
+//
+// Per step and lane: ~46 VALU ops for 32 cells (pk2: ~44 for 16), the stored
+// traceback is 2 bits per cell (pk2: 4) and the hand-off 2 NP bits per column.
+// The traceback reads the (diag, up) bits back: a scalar walk over 64-step x
+// 64-row tiles staged in VGPRs (one v_readlane per bit word and move).
+//
+// Stored layout per band: dword ((s >> 3) * 64 + lane) * 16 + (s & 7) holds the
+// diag bits of step s, + 8 the up bits; a band has 64 * sblocks steps
+// (sblocks = nchunks + 32: the last row runs 2047 columns behind the first).
+#include "nwk_internal.h"
+
+namespace nwk {
+namespace {
+
+typedef unsigned long long u64;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+#define BITS_RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
+constexpr int kBR = kBitsRows;  // rows per band (64 lanes x 32 bits)
+
+__device__ __forceinline__ unsigned long long bits_opaque_zero() {
+  unsigned long long z = 0;
+  asm volatile("" : "+v"(z));
+  return z;
+}
+
+// Polls the granules lanes 0..n-1 hold until every one carries `epoch`
+// (bounded: ~4 s of wall time, or another wave's failure).
+__device__ __noinline__ u64 bits_wait(const u64* p, bool mine, unsigned epoch, u64 v, unsigned* err) {
+  const u64 t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (__all(!mine || (unsigned)(v >> 32) == epoch)) return v;
+    __builtin_amdgcn_s_sleep(4);
+    if (__hip_atomic_load((gu32*)err, BITS_RLX) != 0u) return 0;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
+      if ((threadIdx.x & 63) == 0) atomicOr(err, 1u);
+      return 0;
+    }
+    // a read-modify-write is performed at the coherence point (no stale L2 copy)
+    if (mine) v = __hip_atomic_fetch_add((gu64*)p, bits_opaque_zero(), BITS_RLX);
+  }
+}
+
+// Eight steps s0 .. s0+7 (s0 % 8 == 0) of one band.
+//   x0, x1   code bit planes of this lane's 32 rows
+//   yp, w    y windows: previous half and this 32-step half (bit 31 - q of w =
+//            code of column s_half - 32 lane + q)
+//   H, V     h and v planes of the previous step
+//   cons     LDS: band-above row, entry (column & 63) * NP + k (bit 31)
+//   ring     LDS: this band's last row, entry (column & 127) * NP + k (bit 31)
+template <int NP, int SR, bool MASK, bool PROD>
+__device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsigned x1, unsigned yp0, unsigned yp1,
+                                           unsigned w0, unsigned w1, unsigned (&H)[NP], unsigned (&V)[NP],
+                                           const unsigned* cons, unsigned* ring, unsigned* st) {
+  unsigned dw[8], uw[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int s = s0 + q;
+    unsigned inj[NP];
+    if constexpr (NP == 4) {
+      const uint4 e = *reinterpret_cast<const uint4*>(cons + (s & 63) * 4);
+      inj[0] = e.x; inj[1] = e.y; inj[2] = e.z; inj[3] = e.w;
+    } else {
+      const uint2 e = *reinterpret_cast<const uint2*>(cons + (s & 63) * 2);
+      inj[0] = e.x; inj[1] = e.y;
+    }
+    const unsigned sh = 31u - (unsigned)(s & 31);
+    const unsigned y0 = __builtin_amdgcn_alignbit(yp0, w0, sh);
+    const unsigned y1 = __builtin_amdgcn_alignbit(yp1, w1, sh);
+    const unsigned mism = (x0 ^ y0) | (x1 ^ y1);
+    const unsigned match = ~mism;
+    unsigned nU[NP], nV[NP], D[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      // lane t-1's plane word (lane 0: the band above), its bit 31 enters at bit 0
+      const unsigned T = (unsigned)__builtin_amdgcn_update_dpp((int)inj[k], (int)H[k], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
+      const unsigned U = __builtin_amdgcn_alignbit(H[k], T, 31);
+      nU[k] = ~U;
+      nV[k] = ~V[k];
+      D[k] = k < SR ? ~0u : (match | U | V[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      unsigned vk = nU[0] & D[k], hk = nV[0] & D[k];
+#pragma unroll
+      for (int j = 1; j + k < NP; ++j) {
+        vk |= nU[j] & D[j + k];
+        hk |= nV[j] & D[j + k];
+      }
+      V[k] = vk;
+      H[k] = hk;
+    }
+    if constexpr (SR < 0) dw[q] = match;
+    else if constexpr (SR >= NP) dw[q] = ~0u;
+    else dw[q] = match | ~D[SR];
+    uw[q] = ~V[0];
+    if constexpr (MASK) {  // columns < 0 keep v = 0 (the left border seen by column 0)
+      const int e = s - 32 * lane;
+      const unsigned M = e >= 31 ? ~0u : (e < 0 ? 0u : (2u << e) - 1u);
+#pragma unroll
+      for (int k = 0; k < NP; ++k) V[k] &= M;
+    }
+    if constexpr (PROD) {  // lane 63 bit 31 = the band's last row at column s - 2047
+      if (lane == 63) {
+        unsigned* e = ring + ((s + 1) & 127) * NP;
+        if constexpr (NP == 4) *reinterpret_cast<uint4*>(e) = make_uint4(H[0], H[1], H[2], H[3]);
+        else *reinterpret_cast<uint2*>(e) = make_uint2(H[0], H[1]);
+      }
+    }
+  }
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(u4{dw[0], dw[1], dw[2], dw[3]}, reinterpret_cast<u4*>(st));
+  __builtin_nontemporal_store(u4{dw[4], dw[5], dw[6], dw[7]}, reinterpret_cast<u4*>(st + 4));
+  __builtin_nontemporal_store(u4{uw[0], uw[1], uw[2], uw[3]}, reinterpret_cast<u4*>(st + 8));
+  __builtin_nontemporal_store(u4{uw[4], uw[5], uw[6], uw[7]}, reinterpret_cast<u4*>(st + 12));
+}
+
+// Traceback of one pair from (m, n) over the stored (diag, up) bits.  A tile
+// is 64 steps (lane L holds step ts - L) of two row-lanes (tt and tt - 1),
+// four dwords per lane; the walk reads one bit word per move by v_readlane.
+#define BITS_PROG(v)                                                                                         \
+  do {                                                                                                       \
+    if (prog && lane == 0) __hip_atomic_store((gu32*)prog, (unsigned)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
+  } while (0)
+
+__device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd, unsigned char* obuf, int lane,
+                                           unsigned* prog) {
+  const int64_t bdw = (int64_t)pd.sblocks * 8192;
+  const unsigned* mat = a.mat + pd.mat_off;
+  uint8_t* ops = a.ops + pd.ops_off;
+  const unsigned ob = (unsigned)(uintptr_t)obuf;
+  int Lc = 0, flushed = 0;
+  auto flush = [&](int upto) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int from = flushed & ~3;
+    for (int o = from + 4 * lane; o < upto; o += 256) {
+      unsigned v;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ob + (unsigned)(o & 255)) : "memory");
+      *reinterpret_cast<unsigned*>(ops + o) = v;
+    }
+    flushed = upto;
+  };
+  // position: band b, band row r (0..2047, -1 = the row above the band), column c (0-based)
+  int b = (pd.m - 1) / kBR, r = (pd.m - 1) % kBR, c = pd.n - 1;
+  int tb = -1, ts = 0, tt = 0;
+  unsigned vd0 = 0, vu0 = 0, vd1 = 0, vu1 = 0;
+  bool bad = false;
+  while (c >= 0 && (b > 0 || r >= 0)) {
+    if (r < 0) {  // into the band above
+      --b;
+      r += kBR;
+    }
+    int t = r >> 5;
+    int s = c + r;
+    BITS_PROG(0x50000000u | ((unsigned)(Lc & 0xfff) << 16) | ((unsigned)(r & 0xff) << 8) | (unsigned)(c & 0xff));
+    if (b != tb || s > ts || s <= ts - 64 || (t != tt && t != tt - 1)) {
+      tb = b;
+      ts = s;
+      tt = t;
+      const int sl = s - lane;
+      vd0 = vu0 = vd1 = vu1 = 0;
+      if (sl >= 0) {
+        const unsigned* p0 = mat + (int64_t)b * bdw + ((int64_t)(sl >> 3) * 64 + t) * 16 + (sl & 7);
+        vd0 = __builtin_nontemporal_load(p0);
+        vu0 = __builtin_nontemporal_load(p0 + 8);
+        if (t > 0) {
+          vd1 = __builtin_nontemporal_load(p0 - 16);
+          vu1 = __builtin_nontemporal_load(p0 - 8);
+        }
+      }
+    }
+    // walk inside the tile
+    for (;;) {
+      // straight-line uniform code: one select per word, one v_readlane each
+      const int L = __builtin_amdgcn_readfirstlane(ts - s);
+      const bool hi = __builtin_amdgcn_readfirstlane(t - tt) == 0;
+      const unsigned vds = hi ? vd0 : vd1, vus = hi ? vu0 : vu1;
+      const unsigned d = (unsigned)__builtin_amdgcn_readlane((int)vds, L);
+      const unsigned u = (unsigned)__builtin_amdgcn_readlane((int)vus, L);
+      const int bit = r & 31;
+      unsigned op;
+      if ((d >> bit) & 1u) {
+        op = 'D';
+        --r;
+        --c;
+        s -= 2;
+      } else if ((u >> bit) & 1u) {
+        op = 'U';
+        --r;
+        s -= 1;
+      } else {
+        op = 'L';
+        --c;
+        s -= 1;
+      }
+      asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(op) : "memory");
+      ++Lc;
+      if (Lc - flushed >= 192) flush(Lc & ~3);
+      if (c < 0 || r < 0) break;
+      t = r >> 5;
+      if (s <= ts - 64 || (t != tt && t != tt - 1)) break;
+    }
+    if (Lc > pd.m + pd.n) {
+      bad = true;
+      break;
+    }
+  }
+  if (bad && lane == 0) atomicOr(a.err, 16u);
+  flush(Lc);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) {
+    a.oplen[pd.slot] = Lc;
+    // the walk ends on the border: row b * 2048 + r + 1, column c + 1
+    a.endij[pd.slot] = make_int2(b * kBR + r + 1, c + 1);
+  }
+}
+
+template <int NP, int SR>
+__global__ __launch_bounds__(256) void nw_align_bits(FillArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned cons_all[4][64 * NP];
+  __shared__ __attribute__((aligned(16))) unsigned ring_all[4][128 * NP];
+  __shared__ __attribute__((aligned(16))) unsigned char obuf_all[4][256];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  unsigned* prog = a.prog ? a.prog + blockIdx.x * 4 + wid : nullptr;  // NWK_WATCHDOG markers
+  unsigned* cons = cons_all[wid];
+  unsigned* ring = ring_all[wid];
+  constexpr int NG = 2 * NP;  // granules per 64-column chunk
+
+  for (;;) {
+    unsigned tk = 0;
+    if (lane == 0) tk = atomicAdd(a.counter, 1u);
+    tk = __builtin_amdgcn_readfirstlane(tk);
+    BITS_PROG(0x10000000u | tk);
+    if (tk >= (unsigned)a.ntasks) { BITS_PROG(0x60000000u); return; }
+    if (__hip_atomic_load((gu32*)a.err, BITS_RLX) != 0u) return;
+    const int2 task = a.tasks[tk];
+    const PairDesc pd = a.pairs[task.x];
+    const int band = task.y;
+    const int R0 = band * kBR;
+    // code bit planes of rows R0 + 32 lane + b (rows past m: code 0, never traced)
+    unsigned x0 = 0, x1 = 0;
+    {
+      const int base = R0 + 32 * lane;
+      const int nv = pd.m - base;
+      const uint8_t* xc = a.codes + pd.x_off + base;
+#pragma unroll
+      for (int b = 0; b < 32; ++b) {
+        const unsigned cd = b < nv ? (unsigned)xc[b] : 0u;
+        x0 |= (cd & 1u) << b;
+        x1 |= ((cd >> 1) & 1u) << b;
+      }
+    }
+    unsigned H[NP], V[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) H[k] = V[k] = 0u;
+    const bool from_above = band > 0;
+    const bool to_below = band + 1 < pd.nbands;
+    const int nch = pd.nchunks, nsb = pd.sblocks;
+    const u64* gin = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)(from_above ? band - 1 : 0) * nch * NG;
+    u64* gout = a.bnd + pd.bnd_off + (int64_t)band * nch * NG;
+    unsigned* mb = a.mat + pd.mat_off + (int64_t)band * nsb * 8192 + lane * 16;
+    // y windows: lane t's window for the half starting at step s_h is position s_h - 32 t
+    const unsigned* ywp = a.yw + 2 * (pd.e_off - 32 * (int64_t)lane);
+    unsigned yp0 = 0, yp1 = 0;
+    unsigned wa0 = ywp[0], wa1 = ywp[1], wb0 = ywp[64], wb1 = ywp[65];
+    const bool gl = lane < NG;
+    u64 g = 0;
+    if (from_above && gl) g = __hip_atomic_load((gu64*)(gin + lane), BITS_RLX);
+    bool ok = true;
+
+    for (int sb = 0; sb < nsb; ++sb) {
+      BITS_PROG(0x20000000u | (unsigned)sb);
+      // --- band-above row for columns 64 sb .. 64 sb + 63 -> cons
+      if (from_above && sb < nch) {
+        if (!__all(!gl || (unsigned)(g >> 32) == a.epoch)) {
+          g = bits_wait(gin + (int64_t)sb * NG + lane, gl, a.epoch, g, a.err);
+          if (!__all(!gl || (unsigned)(g >> 32) == a.epoch)) { ok = false; break; }
+        }
+        const unsigned dat = (unsigned)g;
+        unsigned e[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+          const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)dat, 2 * k);
+          const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)dat, 2 * k + 1);
+          const unsigned w = lane < 32 ? lo : hi;
+          e[k] = (w >> (lane & 31)) << 31;
+        }
+        if constexpr (NP == 4) *reinterpret_cast<uint4*>(cons + lane * 4) = make_uint4(e[0], e[1], e[2], e[3]);
+        else *reinterpret_cast<uint2*>(cons + lane * 2) = make_uint2(e[0], e[1]);
+      } else if (sb == 0 || sb == nch) {  // top border (band 0) / past the last chunk: zeros
+        if constexpr (NP == 4) *reinterpret_cast<uint4*>(cons + lane * 4) = make_uint4(0, 0, 0, 0);
+        else *reinterpret_cast<uint2*>(cons + lane * 2) = make_uint2(0, 0);
+      }
+      if (from_above && sb + 1 < nch && gl) g = __hip_atomic_load((gu64*)(gin + (int64_t)(sb + 1) * NG + lane), BITS_RLX);
+      // next super-block's windows
+      const unsigned* wn = ywp + 128 * (sb + 1);
+      const unsigned na0 = wn[0], na1 = wn[1], nb0 = wn[64], nb1 = wn[65];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+
+      const bool mask = sb < 32;
+      const bool prod = to_below && sb >= 31;
+#pragma unroll
+      for (int blk = 0; blk < 8; ++blk) {
+        const int s0 = 64 * sb + 8 * blk;
+        const unsigned w0 = blk < 4 ? wa0 : wb0, w1 = blk < 4 ? wa1 : wb1;
+        unsigned* st = mb + (int64_t)(s0 >> 3) * 1024;
+        if (mask) {
+          if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st);
+          else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st);
+        } else {
+          if (prod) bits_block<NP, SR, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st);
+          else bits_block<NP, SR, false, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st);
+        }
+        if ((blk & 3) == 3) {  // end of a 32-step half: its window becomes the previous one
+          yp0 = w0;
+          yp1 = w1;
+        }
+      }
+      wa0 = na0; wa1 = na1; wb0 = nb0; wb1 = nb1;
+      // --- publish chunk q = sb - 32 of this band's last row (complete after this super-block)
+      if (to_below && sb >= 32 && sb - 32 < nch) {
+        const int q = sb - 32;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const unsigned* e = ring + ((64 * q + lane) & 127) * NP;
+        unsigned val = 0;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+          const u64 m64 = __ballot((e[k] >> 31) != 0u);
+          val = lane == 2 * k ? (unsigned)m64 : val;
+          val = lane == 2 * k + 1 ? (unsigned)(m64 >> 32) : val;
+        }
+        if (gl) __hip_atomic_store((gu64*)(gout + (int64_t)q * NG + lane), ((u64)a.epoch << 32) | val, BITS_RLX);
+      }
+    }
+    BITS_PROG(0x30000000u);
+    if (!ok) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add((gu32*)(a.done + pd.slot), 1u, BITS_RLX);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev + 1u == (unsigned)pd.nbands) {  // the pair's last band: every band has released
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (a.dbg_notrace) {
+        if (lane == 0) { a.oplen[pd.slot] = 0; a.endij[pd.slot] = make_int2(pd.m, pd.n); }
+      } else {
+        BITS_PROG(0x40000000u);
+        trace_bits(a, pd, obuf_all[wid], lane, prog);
+        BITS_PROG(0x56000000u);
+      }
+    }
+  }
+}
+
+template <int NP, int SR>
+hipError_t bits_launch(const FillArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((nw_align_bits<NP, SR>), dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int NP, int SR>
+int bits_occ() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&nw_align_bits<NP, SR>), 256, 0) !=
+      hipSuccess)
+    return 1;
+  return n > 0 ? n : 1;
+}
+
+}  // namespace
+
+// SR = 2 pgap - pxy clamped to [-1, NP]: the mismatch score's thermometer level
+int bits_sr(int pxy, int pgap) {
+  const int np = 2 * pgap, sr = np - pxy;
+  return sr < -1 ? -1 : (sr > np ? np : sr);
+}
+
+bool bits_admissible(int pxy, int pgap, int alpha) { return pxy >= 0 && (pgap == 1 || pgap == 2) && alpha <= 4; }
+
+hipError_t launch_bits(const FillArgs& a, int pxy, int pgap, int grid, hipStream_t s) {
+  const int sr = bits_sr(pxy, pgap);
+  if (pgap == 1) {
+    switch (sr) {
+      case -1: return bits_launch<2, -1>(a, grid, s);
+      case 0: return bits_launch<2, 0>(a, grid, s);
+      case 1: return bits_launch<2, 1>(a, grid, s);
+      default: return bits_launch<2, 2>(a, grid, s);
+    }
+  }
+  if (pgap == 2) {
+    switch (sr) {
+      case -1: return bits_launch<4, -1>(a, grid, s);
+      case 0: return bits_launch<4, 0>(a, grid, s);
+      case 1: return bits_launch<4, 1>(a, grid, s);
+      case 2: return bits_launch<4, 2>(a, grid, s);
+      case 3: return bits_launch<4, 3>(a, grid, s);
+      default: return bits_launch<4, 4>(a, grid, s);
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+int bits_blocks_per_cu(int pgap) { return pgap == 1 ? bits_occ<2, 1>() : bits_occ<4, 1>(); }
+
+}  // namespace nwk

@@ -26,7 +26,9 @@ enum Mode : int {
   kPacked2 = 5,  // kPacked with two bands per wave (band pairs), layout LY 2
   kProfileDP = 6,  // profile-profile sum-of-pairs DP of the progressive MSA, 4-bit codes
   kAffinePk = 7,   // kAffine on band pairs as int16 pairs (nw_align_pka), layout LY 2, profile codes
+  kBits = 8,       // bit-sliced difference planes (nw_align_bits, nwk_bits.hip): 2048-row bands, 2-bit traceback
 };
+constexpr int kBitsRows = 2048;  // kBits: rows per band (64 lanes x 32 bits)
 
 // One pair of the batch.  All offsets are element offsets into the
 // batch-level arrays passed to the kernels.
@@ -88,6 +90,7 @@ struct FillArgs {
   int ntjobs;              // jobs the batch will produce
   const int* prow;         // kProfileDP: per X column (DP row) 8 ints {rc[0..5], gx, H[i][0]} at pairs[].x_off
   const int* pcol;         // kProfileDP: per Y column (DP column) 8 ints {cnt[0..5], gy, H[0][j]} at pairs[].y_off
+  const unsigned* yw;      // kBits: per y position p two dwords (code bit planes of y[p .. p+31], y[p] at bit 31), at pairs[].e_off
 };
 constexpr int kProfSyms = 6;  // kProfileDP: symbols + gap per column profile
 
@@ -114,6 +117,10 @@ hipError_t launch_hash(const HashArgs& h, hipStream_t s);
 hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStream_t s);
 hipError_t launch_gather(const FillArgs& a, int npairs, int task_shift, hipStream_t s);
 int fill_blocks_per_cu(int mode, int bits);
+// kBits (nwk_bits.hip)
+bool bits_admissible(int pxy, int pgap, int alpha);
+hipError_t launch_bits(const FillArgs& a, int pxy, int pgap, int grid, hipStream_t s);
+int bits_blocks_per_cu(int pgap);
 
 // Dwords of one band of the stored matrix.
 __host__ __device__ inline int64_t band_dwords(int bits, int sblocks) {

@@ -158,6 +158,9 @@ struct nwk_ctx {
   bool built[2] = {false, false};
   DevBuf d_sel[4];              // selector streams: [hi 0x00, hi 0xff] x [kPacked (lag 1), kPacked2 (lag 64)]
   bool built_sel[4] = {false, false, false, false};
+  std::vector<int64_t> yw_off;  // kBits: y-window index of position 0 per sequence
+  DevBuf d_yw;                  // kBits: 32-column code-plane windows, two dwords per position
+  bool built_yw = false;
 
   // batch buffers
   DevBuf d_work;                // matrices | boundary granules | op strings
@@ -196,6 +199,7 @@ void nwk_ctx_destroy(nwk_ctx* c) {
   for (auto& b : c->d_codes) b.release();
   for (auto& b : c->d_E) b.release();
   for (auto& b : c->d_sel) b.release();
+  c->d_yw.release();
   c->d_work.release();
   c->d_pairs.release(); c->d_tasks.release(); c->d_ctl.release();
   c->d_oplen.release(); c->d_endij.release(); c->d_done.release(); c->d_stamps.release();
@@ -269,6 +273,7 @@ int nwk_set_sequences(nwk_ctx* c, const uint8_t* seqs, const int64_t* offsets, i
   c->has_us = seen[(unsigned char)'_'];
   c->built[0] = c->built[1] = false;
   for (auto& b : c->built_sel) b = false;
+  c->built_yw = false;
   // layout: codes 8-aligned; E / SEL with kEPad entries before column 0 and kETail past the end
   c->c_off.resize(k);
   c->e_off.resize(k);
@@ -350,6 +355,46 @@ int build_sel(nwk_ctx* c, int neg, int lag) {
   return NWK_OK;
 }
 
+// kBits y windows: per position p (kYwFront before column 0 .. kYwTail past
+// the end) two dwords, bit 31 - q of dword k = bit k of code(y[p + q]) (0
+// outside the sequence).  nw_align_bits lane t reads position s_half - 32 t.
+constexpr int64_t kYwFront = kBitsRows + 128, kYwTail = kBitsRows + 512;
+int build_yw(nwk_ctx* c) {
+  if (c->built_yw) return NWK_OK;
+  const int k = c->k;
+  c->yw_off.assign((size_t)k, 0);
+  int64_t tot = 0;
+  for (int s = 0; s < k; ++s) {
+    c->yw_off[s] = tot + kYwFront;
+    tot += kYwFront + (c->off[s + 1] - c->off[s]) + kYwTail;
+  }
+  std::vector<uint32_t> W((size_t)std::max<int64_t>(2 * tot, 2), 0);
+  for (int s = 0; s < k; ++s) {
+    const uint8_t* y = c->seqs.data() + c->off[s];
+    const int64_t L = c->off[s + 1] - c->off[s];
+    uint32_t* w = W.data() + 2 * (c->yw_off[s] - kYwFront);
+    auto code = [&](int64_t t) -> uint32_t { return t >= 0 && t < L ? c->code_of[y[t]] : 0u; };
+    uint32_t w0 = 0, w1 = 0;  // window of position p - 1
+    for (int64_t q = 0; q < 31; ++q) {  // prime: positions p = -kYwFront - 1 .. covers y[p .. p+31]
+      const uint32_t cd = code(-kYwFront - 1 + q);
+      w0 = (w0 << 1) | (cd & 1u);
+      w1 = (w1 << 1) | ((cd >> 1) & 1u);
+    }
+    for (int64_t p = -kYwFront; p < L + kYwTail; ++p) {
+      const uint32_t cd = code(p + 31);  // the window's newest column enters at bit 0
+      w0 = (w0 << 1) | (cd & 1u);
+      w1 = (w1 << 1) | ((cd >> 1) & 1u);
+      w[2 * (p + kYwFront)] = w0;
+      w[2 * (p + kYwFront) + 1] = w1;
+    }
+  }
+  int rc;
+  if ((rc = c->d_yw.ensure(W.size() * 4)) != NWK_OK) return rc;
+  HIP_TRY(hipMemcpy(c->d_yw.p, W.data(), W.size() * 4, hipMemcpyHostToDevice));
+  c->built_yw = true;
+  return NWK_OK;
+}
+
 struct Plan {
   int mode, bits, kind;
   int K0, K1;
@@ -410,9 +455,16 @@ int choose_plan(const nwk_ctx* c, const Scoring& sc, Plan* pl) {
   // 0) pins nw_align / nw_align_pk / nw_align_pk2 for tests and A/B runs; a
   // packed kernel asked for where it is not exact falls back to nw_align.
   static const int packed_env = getenv("NWK_PACKED") ? atoi(getenv("NWK_PACKED")) : 2;
-  const int packed = c->opts.kernel > 0 ? c->opts.kernel - 1 : packed_env;
+  const int packed = c->opts.kernel > 0 && c->opts.kernel < 4 ? c->opts.kernel - 1 : packed_env;
   if (pl->mode == kProfile && pl->bits == 4 && packed > 0 && ((pl->K0 < 0) == (pl->K1 < 0)))
     pl->mode = packed == 1 ? kPacked : kPacked2;
+  // bit-sliced difference planes (nw_align_bits) wherever they apply: pxy >= 0,
+  // pgap in {1, 2}, <= 4 symbols.  opts.kernel 4 (or NWK_BITS=1) asks for it,
+  // 1..3 pin the integer kernels, NWK_BITS=0 disables it under "auto".
+  // pl->bits keeps the profile kernels' width (the linear-space path uses it).
+  static const int bits_env = getenv("NWK_BITS") ? atoi(getenv("NWK_BITS")) : 1;
+  const bool want_bits = c->opts.kernel == 4 || (c->opts.kernel == 0 && bits_env != 0);
+  if (want_bits && c->opts.bits == 0 && bits_admissible(pxy, pgap, c->alpha)) pl->mode = kBits;
   return NWK_OK;
 }
 
@@ -442,7 +494,21 @@ void seg_footprint(PairWork* w, int mode, int E, int NG) {
   w->segctl_b = nt * 4 + nt * NG * 32 + (w->m / 128 + 1) * 32 * 8 + w->njobs * 12;  // records: 32 slots per 128th row
 }
 
+// kBits geometry: 2048-row bands, 64 * (nchunks + 32) steps of 2 x 64 dwords,
+// 2 NP <= 8 granules per 64-column chunk of each band's last row
+inline int bits_sblocks(int64_t nch) { return (int)(nch + 32); }
+constexpr int kBitsGranPerChunk = 8;
+
 void footprint(PairWork* w, int bits, int mode, bool affine) {
+  if (mode == kBits) {
+    const int64_t nb = ceil_div(w->m, kBitsRows), nch = ceil_div(w->n, 64);
+    w->segops_b = w->segctl_b = 0;
+    w->spec = 0;
+    w->mat_dw = nb * bits_sblocks(nch) * 8192;
+    w->bnd_gr = (nb - 1) * nch * kBitsGranPerChunk;
+    w->ops_b = round_up((int64_t)w->m + w->n, 16);
+    return;
+  }
   const int64_t nb = ceil_div(w->m, kBandRows);
   const int64_t nch = ceil_div(w->n, 64);
   const int64_t nt = tasks_of(mode, nb);
@@ -589,7 +655,7 @@ LinGeo lin_geo(const Plan& pl, const PairWork& w, int G) {
 
 Plan lin_plan(const Plan& pl0) {
   Plan pl = pl0;
-  if (pl.mode == kPacked || pl.mode == kPacked2) pl.mode = kProfile;  // same bits (4), codes and K0/K1
+  if (pl.mode == kPacked || pl.mode == kPacked2 || pl.mode == kBits) pl.mode = kProfile;  // same bits, codes, K0/K1
   return pl;
 }
 
@@ -782,7 +848,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       if (w.m > 0 && w.n > 0) t2 += ceil_div(w.m, 2 * kBandRows);
     if (t2 < 8 * (int64_t)c->cus) pl.mode = kPacked;  // (2048 on 256 CUs; the kernels tie near there)
   }
-  st.bits = pl.bits;
+  st.bits = pl.mode == kBits ? 2 : pl.bits;
   st.mode = pl.mode;
   int rc;
   HIP_TRY(hipSetDevice(c->device));
@@ -807,6 +873,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   }
   if (!dp.empty()) {
     if ((rc = build_encoding(c, pl.kind)) != NWK_OK) return rc;
+    if (pl.mode == kBits && (rc = build_yw(c)) != NWK_OK) return rc;
     if ((pl.mode == kPacked || band_pairs(pl.mode)) &&
         (rc = build_sel(c, pl.K0 < 0 ? 1 : 0, band_pairs(pl.mode) ? 64 : 1)) != NWK_OK)
       return rc;
@@ -846,7 +913,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       acc += (double)w.m * w.n;
     }
   }
-  int bpc = fill_blocks_per_cu(pl.mode, pl.bits);
+  int bpc = pl.mode == kBits ? bits_blocks_per_cu(sc.pgap) : fill_blocks_per_cu(pl.mode, pl.bits);
   // waves per SIMD: nw_align_pk2 measured best at 2 (band chains run at the
   // pace of their slowest member; more waves per SIMD only add waiting);
   // NWK_BPC overrides (experiments)
@@ -972,15 +1039,15 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       PairDesc& d = pd[q];
       d.x_off = c->c_off[w.i];
       d.y_off = c->c_off[w.j];
-      d.e_off = c->e_off[w.j];
+      d.e_off = pl.mode == kBits ? c->yw_off[w.j] : c->e_off[w.j];
       d.mat_off = mat_base_b / 4 + mo;
       d.bnd_off = bo;
       d.ops_off = ops_base_b + oo;
       d.m = w.m;
       d.n = w.n;
-      d.nbands = (int)ceil_div(w.m, kBandRows);
+      d.nbands = (int)ceil_div(w.m, pl.mode == kBits ? kBitsRows : kBandRows);
       d.nchunks = (int)ceil_div(w.n, 64);
-      d.sblocks = sblocks_of(pl.mode, d.nchunks);
+      d.sblocks = pl.mode == kBits ? bits_sblocks(d.nchunks) : sblocks_of(pl.mode, d.nchunks);
       d.slot = q;
       d.spec_every = w.spec;
       d.nguess = w.nguess;
@@ -1066,6 +1133,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.dbg_notrace = (getenv("NWK_AFF_NOTRACE") || getenv("NWK_NOTRACE")) ? 1 : 0;
     fa.lin_mode = 0;
     fa.prog = nullptr;
+    fa.yw = pl.mode == kBits ? c->d_yw.as<unsigned>() : nullptr;
     if (getenv("NWK_WATCHDOG")) {
       if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;
       HIP_TRY(hipMemsetAsync(c->d_prog.p, 0, 4 * (size_t)(grid + 1) * 4, c->stream));
@@ -1103,7 +1171,10 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       fflush(stderr);
     }
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-    HIP_TRY(launch_fill(pl.mode, pl.bits, fa, std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
+    if (pl.mode == kBits)
+      HIP_TRY(launch_bits(fa, sc.pxy, sc.pgap, (int)std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
+    else
+      HIP_TRY(launch_fill(pl.mode, pl.bits, fa, std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     if (seg) HIP_TRY(launch_gather(fa, np, pl.mode == kPacked2 ? 1 : 0, c->stream));  // segment chains -> op strings
     if (devhash) {

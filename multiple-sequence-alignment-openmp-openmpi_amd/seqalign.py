@@ -24,10 +24,10 @@ LIB_PATH = os.path.join(HERE, "lib", "libnwk.so")
 NWK_OK = 0
 ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "EKERNEL", -5: "ECOMM"}
 MODES = {0: "profile", 1: "compare", 2: "literal", 3: "affine", 4: "packed-profile", 5: "packed-band-pairs",
-         7: "packed-affine-band-pairs"}
+         7: "packed-affine-band-pairs", 8: "bit-sliced-planes"}
 # fill kernel of each mode (csrc/nwk_kernels.hip), as rocprofv3 names it
 KERNELS = {0: "nw_align", 1: "nw_align", 2: "nw_align", 3: "nw_align_affine", 4: "nw_align_pk", 5: "nw_align_pk2",
-           7: "nw_align_pka"}
+           7: "nw_align_pka", 8: "nw_align_bits"}
 
 
 class NwkError(RuntimeError):
@@ -147,7 +147,7 @@ class Engine:
 
     FINALIZE = {"auto": 0, "host": 1, "device": 2}
 
-    KERNEL = {"auto": 0, "nw_align": 1, "nw_align_pk": 2, "nw_align_pk2": 3}
+    KERNEL = {"auto": 0, "nw_align": 1, "nw_align_pk": 2, "nw_align_pk2": 3, "nw_align_bits": 4}
 
     def __init__(self, device=0, bits=0, workspace_bytes=0, host_threads=0, verbose=False, finalize="auto",
                  linear_space=0, kernel="auto"):
@@ -162,7 +162,7 @@ class Engine:
         # linear-space traceback: 0 only where the matrix does not fit,
         # -1 never, G > 0 every pair with G bands per recompute group
         o.linear_space = linear_space
-        # linear fill kernel (tests / A/B): "auto", "nw_align", "nw_align_pk", "nw_align_pk2"
+        # linear fill kernel (tests / A/B): "auto", "nw_align", "nw_align_pk", "nw_align_pk2", "nw_align_bits"
         o.kernel = self.KERNEL[kernel]
         self._ctx = ctypes.c_void_p()
         _check(self.lib.nwk_ctx_create(ctypes.byref(o), ctypes.byref(self._ctx)))
