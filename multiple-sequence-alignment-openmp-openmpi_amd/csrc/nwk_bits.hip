@@ -28,9 +28,13 @@
 // The traceback reads the (diag, up) bits back: a scalar walk over 64-step x
 // 64-row tiles staged in VGPRs (one v_readlane per bit word and move).
 //
-// Stored layout per band: dword ((s >> 3) * 64 + lane) * 16 + (s & 7) holds the
-// diag bits of step s, + 8 the up bits; a band has 64 * sblocks steps
-// (sblocks = nchunks + 32: the last row runs 2047 columns behind the first).
+// Stored layout per band: 8-step block B = s >> 3 owns 1024 dwords; the diag
+// bits of step s for lane t sit at dword B * 1024 + ((s & 7) >> 2) * 256 +
+// 4 t + (s & 3), the up bits 512 dwords further.  Each of a block's four
+// 16-byte stores thus writes 1 KB contiguous across the wave (whole lines:
+// a lane-major 64-byte-stride layout wrote partial lines at ~1.1 TB/s).  A
+// band has 64 * sblocks steps (sblocks = nchunks + 32: the last row runs 2047
+// columns behind the first).
 #include "nwk_internal.h"
 
 namespace nwk {
@@ -78,17 +82,26 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
                                            unsigned w0, unsigned w1, unsigned (&H)[NP], unsigned (&V)[NP],
                                            const unsigned* cons, unsigned* ring, unsigned* st) {
   unsigned dw[8], uw[8];
+  // the band-above entries are read one step ahead (an LDS read's latency
+  // would otherwise sit on every step's dependence chain)
+  unsigned injn[NP];
+  auto read_inj = [&](int s) {
+    if constexpr (NP == 4) {
+      const uint4 e = *reinterpret_cast<const uint4*>(cons + (s & 63) * 4);
+      injn[0] = e.x; injn[1] = e.y; injn[2] = e.z; injn[3] = e.w;
+    } else {
+      const uint2 e = *reinterpret_cast<const uint2*>(cons + (s & 63) * 2);
+      injn[0] = e.x; injn[1] = e.y;
+    }
+  };
+  read_inj(s0);
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int s = s0 + q;
     unsigned inj[NP];
-    if constexpr (NP == 4) {
-      const uint4 e = *reinterpret_cast<const uint4*>(cons + (s & 63) * 4);
-      inj[0] = e.x; inj[1] = e.y; inj[2] = e.z; inj[3] = e.w;
-    } else {
-      const uint2 e = *reinterpret_cast<const uint2*>(cons + (s & 63) * 2);
-      inj[0] = e.x; inj[1] = e.y;
-    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) inj[k] = injn[k];
+    if (q < 7) read_inj(s + 1);
     const unsigned sh = 31u - (unsigned)(s & 31);
     const unsigned y0 = __builtin_amdgcn_alignbit(yp0, w0, sh);
     const unsigned y1 = __builtin_amdgcn_alignbit(yp1, w1, sh);
@@ -135,9 +148,9 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
   }
   typedef unsigned u4 __attribute__((ext_vector_type(4)));
   __builtin_nontemporal_store(u4{dw[0], dw[1], dw[2], dw[3]}, reinterpret_cast<u4*>(st));
-  __builtin_nontemporal_store(u4{dw[4], dw[5], dw[6], dw[7]}, reinterpret_cast<u4*>(st + 4));
-  __builtin_nontemporal_store(u4{uw[0], uw[1], uw[2], uw[3]}, reinterpret_cast<u4*>(st + 8));
-  __builtin_nontemporal_store(u4{uw[4], uw[5], uw[6], uw[7]}, reinterpret_cast<u4*>(st + 12));
+  __builtin_nontemporal_store(u4{dw[4], dw[5], dw[6], dw[7]}, reinterpret_cast<u4*>(st + 256));
+  __builtin_nontemporal_store(u4{uw[0], uw[1], uw[2], uw[3]}, reinterpret_cast<u4*>(st + 512));
+  __builtin_nontemporal_store(u4{uw[4], uw[5], uw[6], uw[7]}, reinterpret_cast<u4*>(st + 768));
 }
 
 // Traceback of one pair from (m, n) over the stored (diag, up) bits.  A tile
@@ -185,12 +198,13 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
       const int sl = s - lane;
       vd0 = vu0 = vd1 = vu1 = 0;
       if (sl >= 0) {
-        const unsigned* p0 = mat + (int64_t)b * bdw + ((int64_t)(sl >> 3) * 64 + t) * 16 + (sl & 7);
+        const unsigned* p0 =
+            mat + (int64_t)b * bdw + (int64_t)(sl >> 3) * 1024 + ((sl & 7) >> 2) * 256 + t * 4 + (sl & 3);
         vd0 = __builtin_nontemporal_load(p0);
-        vu0 = __builtin_nontemporal_load(p0 + 8);
+        vu0 = __builtin_nontemporal_load(p0 + 512);
         if (t > 0) {
-          vd1 = __builtin_nontemporal_load(p0 - 16);
-          vu1 = __builtin_nontemporal_load(p0 - 8);
+          vd1 = __builtin_nontemporal_load(p0 - 4);
+          vu1 = __builtin_nontemporal_load(p0 + 508);
         }
       }
     }
@@ -284,7 +298,7 @@ __global__ __launch_bounds__(256) void nw_align_bits(FillArgs a) {
     const int nch = pd.nchunks, nsb = pd.sblocks;
     const u64* gin = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)(from_above ? band - 1 : 0) * nch * NG;
     u64* gout = a.bnd + pd.bnd_off + (int64_t)band * nch * NG;
-    unsigned* mb = a.mat + pd.mat_off + (int64_t)band * nsb * 8192 + lane * 16;
+    unsigned* mb = a.mat + pd.mat_off + (int64_t)band * nsb * 8192 + lane * 4;
     // y windows: lane t's window for the half starting at step s_h is position s_h - 32 t
     const unsigned* ywp = a.yw + 2 * (pd.e_off - 32 * (int64_t)lane);
     unsigned yp0 = 0, yp1 = 0;

@@ -10,6 +10,7 @@ P=multiple-sequence-alignment-openmp-openmpi_amd
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 $*"
 /opt/rocm/bin/hipcc $F -c $P/csrc/nwk_kernels.hip -o $out/obj/k.o
 /opt/rocm/bin/hipcc $F -c $P/csrc/nwk_hash.hip -o $out/obj/h.o
+/opt/rocm/bin/hipcc $F -c $P/csrc/nwk_bits.hip -o $out/obj/b.o
 /opt/rocm/bin/hipcc $F -c $P/csrc/nwk_runtime.cpp -o $out/obj/r.o
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -c $P/csrc/sha512.cpp -o $out/obj/s.o
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $out/libnwk.so $out/obj/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib

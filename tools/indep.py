@@ -4,6 +4,8 @@ import os, sys, time
 sys.path.insert(0, "multiple-sequence-alignment-openmp-openmpi_amd")
 import numpy as np
 import seqalign
+if os.environ.get("LIB"):
+    seqalign.load_library(os.path.join(os.environ["LIB"], "libnwk.so"))
 args = [int(a) for a in sys.argv[1:]]
 rng = np.random.default_rng(1)
 for q in range(0, len(args), 3):
