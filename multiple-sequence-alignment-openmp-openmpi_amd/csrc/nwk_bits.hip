@@ -60,7 +60,7 @@ __device__ __noinline__ u64 bits_wait(const u64* p, bool mine, unsigned epoch, u
   for (;;) {
     if (__all(!mine || (unsigned)(v >> 32) == epoch)) return v;
     __builtin_amdgcn_s_sleep(4);
-    if (__hip_atomic_load((gu32*)err, BITS_RLX) != 0u) return 0;
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)err, BITS_RLX)) != 0u) return 0;
     if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
       if ((threadIdx.x & 63) == 0) atomicOr(err, 1u);
       return 0;
@@ -272,7 +272,8 @@ __global__ __launch_bounds__(256) void nw_align_bits(FillArgs a) {
     tk = __builtin_amdgcn_readfirstlane(tk);
     BITS_PROG(0x10000000u | tk);
     if (tk >= (unsigned)a.ntasks) { BITS_PROG(0x60000000u); return; }
-    if (__hip_atomic_load((gu32*)a.err, BITS_RLX) != 0u) return;
+    // wave-uniform exit (a per-lane load would make the task loop divergent)
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)a.err, BITS_RLX)) != 0u) return;
     const int2 task = a.tasks[tk];
     const PairDesc pd = a.pairs[task.x];
     const int band = task.y;
