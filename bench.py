@@ -390,7 +390,10 @@ def main():
         "dtype": "int16x2-relative (int32-exact results, 4-bit mod-16 traceback storage)"
                  if st["mode"] in (4, 5) else
                  "int16x2-relative, x4 with 2-bit source tags (int32-exact results, 4-bit traceback codes)"
-                 if st["mode"] == 7 else ("int32" if st["bits"] == 32 else
+                 if st["mode"] == 7 else
+                 "u32 bit planes (bit-sliced: 32 cells per VALU op, 2*pgap thermometer planes of the "
+                 "G-space differences; int32-exact results, 2-bit traceback storage)"
+                 if st["mode"] == 8 else ("int32" if st["bits"] == 32 else
                                               "int32 (%d-bit mod-2^W traceback storage)" % st["bits"]),
         "data": "reference input file (mseq-big13-example.txt)" if args.workload == "big13"
                 else "synthetic (seeded MT19937 ACGT, workloads.py)",

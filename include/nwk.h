@@ -60,8 +60,9 @@ typedef struct nwk_opts {
   int32_t finalize;          /* pair finalize (rows, penalty, SHA-512): 0 auto, 1 host, 2 device (nw_hash) */
   int32_t linear_space;      /* linear-space traceback: 0 = only for pairs whose matrix exceeds
                                 the HBM budget, -1 = never, G > 0 = every pair, G bands per recompute group */
-  int32_t kernel;            /* linear fill kernel: 0 auto, 1 nw_align, 2 nw_align_pk, 3 nw_align_pk2 (a packed
-                                kernel where it is not exact -- W > 4 or mixed-sign K -- falls back to nw_align) */
+  int32_t kernel;            /* linear fill kernel: 0 auto (nw_align_bits where admissible: pxy >= 0, pgap 1 or 2,
+                                <= 4 symbols), 1 nw_align, 2 nw_align_pk, 3 nw_align_pk2, 4 nw_align_bits (a
+                                kernel where it is not exact -- W > 4, mixed-sign K, pgap > 2 -- falls back) */
   int32_t reserved[2];
 } nwk_opts;
 
@@ -73,7 +74,8 @@ typedef struct nwk_stats {
   int64_t matrix_bytes;      /* HBM bytes of the stored DP matrices */
   int32_t batches;           /* workspace batches used */
   int32_t bits;              /* storage width used */
-  int32_t mode;              /* 0 = profile, 1 = compare, 2 = literal, 3 = affine, 4 = packed profile, 5 = packed band pairs */
+  int32_t mode;              /* 0 = profile, 1 = compare, 2 = literal, 3 = affine, 4 = packed profile, 5 = packed band
+                                pairs, 7 = packed affine band pairs, 8 = bit-sliced planes */
   int32_t fill_launches;     /* fill-kernel launches in the call */
   int32_t device_finalized;  /* batches whose pairs were finalized on the device */
   int32_t linear_space_pairs; /* pairs aligned with the linear-space traceback */

@@ -98,6 +98,74 @@ def test_forced_widths_and_alphabets(bits, alpha):
     assert [x.tobytes().hex() for x in hs] == ohs
 
 
+BITS_PENALTIES = [(p, 2) for p in range(0, 6)] + [(p, 1) for p in range(0, 4)] + [(9, 2), (7, 1)]
+
+
+@pytest.mark.parametrize("pxy,pgap", BITS_PENALTIES)
+def test_bits_kernel_every_mismatch_level(pxy, pgap):
+    """nw_align_bits (csrc/nwk_bits.hip) at every thermometer level of the
+    mismatch score SR = 2 pgap - pxy (clamped to [-1, 2 pgap]), on lengths that
+    straddle its 32-row lane words, 2048-row bands and 64-column chunks, plus
+    mutated copies (paths off the diagonal); bit-exact against the oracle."""
+    r = random.Random(pxy * 31 + pgap)
+    lens = [1, 31, 33, 2047, 2048, 2049, 4200]
+    genes = [bytes(r.choice(ACGT) for _ in range(L)) for L in lens]
+    genes += _mutants(r, bytes(r.choice(ACGT) for _ in range(3000)), 2, ACGT)
+    with seqalign.Engine(device=0, kernel="nw_align_bits") as e:
+        e.set_sequences(genes)
+        pen, hs = e.align_pairs(_all_ids(len(genes)), pxy, pgap)
+        assert e.stats()["mode"] == 8, "nw_align_bits expected"
+    _, opens, ohs = oracle.all_pairs(genes, pxy, pgap)
+    assert [int(v) for v in pen] == opens
+    assert [x.tobytes().hex() for x in hs] == ohs
+
+
+_ORDER_SCRIPT = r"""
+import json, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import seqalign
+genes = [bytes.fromhex(g) for g in json.loads(sys.stdin.read())]
+k = len(genes)
+out = []
+for pxy, pgap in ((3, 2), (5, 1)):
+    with seqalign.Engine(device=0, workspace_bytes=64 << 20) as e:
+        e.set_sequences(genes)
+        pen, hs = e.align_pairs(np.arange(k * (k - 1) // 2, dtype=np.int64), pxy, pgap)
+        st = e.stats()
+    out.append({"mode": st["mode"], "batches": st["batches"], "pen": [int(v) for v in pen],
+                "hs": [x.tobytes().hex() for x in hs]})
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("order", ["0", "1", "3"])
+def test_bits_kernel_task_orders_multi_batch(order):
+    """nw_align_bits under each task order of the runtime (NWK_ORDER: 0
+    pair-major, 1 band-major -- the default when a batch holds more than two
+    rounds of tasks per wave slot, as C3/C4 do --, g >= 2 groups of g pairs)
+    with a small workspace, so several batches reuse the granule region.  The
+    order is read once per process, hence the child process.  Bit-exact vs the
+    oracle on 3/2 and 5/1 (the reference's two penalty sets)."""
+    import json
+    import subprocess
+    import sys
+
+    r = random.Random(77)
+    genes = _rand_genes(r, 7, 5000, 7000, ACGT)
+    env = dict(os.environ, NWK_ORDER=order)
+    res = subprocess.run([sys.executable, "-c", _ORDER_SCRIPT, os.path.dirname(seqalign.__file__)],
+                         input=json.dumps([g.hex() for g in genes]).encode(), env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
+    assert res.returncode == 0, res.stderr.decode()[-2000:]
+    out = json.loads(res.stdout.decode().strip().splitlines()[-1])
+    for (pxy, pgap), o in zip(((3, 2), (5, 1)), out):
+        assert o["mode"] == 8 and o["batches"] > 1
+        _, opens, ohs = oracle.all_pairs(genes, pxy, pgap)
+        assert o["pen"] == opens
+        assert o["hs"] == ohs
+
+
 def test_subset_and_order_of_pair_ids(engine):
     r = random.Random(5)
     genes = _rand_genes(r, 7, 50, 900, ACGT)

@@ -112,7 +112,7 @@ def _edge_cases():
     return json.load(open(f))["cases"] if os.path.exists(f) else []
 
 
-@pytest.mark.parametrize("kernel", ["auto", "nw_align_pk", "nw_align_pk2", "nw_align"])
+@pytest.mark.parametrize("kernel", ["auto", "nw_align_pk", "nw_align_pk2", "nw_align", "nw_align_bits"])
 @pytest.mark.parametrize("case", _edge_cases(), ids=lambda c: "pxy%d_pgap%d" % (c["pxy"], c["pgap"]))
 def test_int16_edge_penalties_long_ragged(case, kernel):
     """20k-60k ragged pairs at 2*pgap + pxy = 14..15 (the W = 4 limit) with every
@@ -135,3 +135,5 @@ def test_int16_edge_penalties_long_ragged(case, kernel):
     want = {"nw_align_pk": 4, "nw_align_pk2": 5}.get(kernel)
     if want is not None:
         assert mode == (want if uniform else 0), "packed kernel only where its profile bytes sign-extend uniformly"
+    if kernel == "nw_align_bits":
+        assert (mode == 8) == (case["pgap"] in (1, 2)), "bit planes exactly where pgap is 1 or 2"

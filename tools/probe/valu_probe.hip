@@ -56,6 +56,23 @@ __global__ __launch_bounds__(256) void probe(unsigned* out, int iters, unsigned 
     if constexpr (OP == 25) { REP16(BODY2("v_xor_b32")) }
     if constexpr (OP == 26) { REP16(BODY2("v_sub_f32")) }
     if constexpr (OP == 27) { REP16(BODYPK("v_pk_mul_f32")) }
+#define BODYX(INS, SUF)                                                                              \
+  asm volatile(INS " %0, %0, %8, %9 " SUF "\n\t" INS " %1, %1, %8, %9 " SUF "\n\t" INS " %2, %2, %8, %9 " SUF \
+               "\n\t" INS " %3, %3, %8, %9 " SUF "\n\t" INS " %4, %4, %8, %9 " SUF "\n\t" INS " %5, %5, %8, %9 " \
+               SUF "\n\t" INS " %6, %6, %8, %9 " SUF "\n\t" INS " %7, %7, %8, %9 " SUF                             \
+               : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)       \
+               : "v"(b), "v"(c));
+#define BODYDPP(CTL)                                                                               \
+  asm volatile("v_mov_b32_dpp %0, %8 " CTL "\n\tv_mov_b32_dpp %1, %8 " CTL "\n\tv_mov_b32_dpp %2, %8 " CTL       \
+               "\n\tv_mov_b32_dpp %3, %8 " CTL "\n\tv_mov_b32_dpp %4, %8 " CTL "\n\tv_mov_b32_dpp %5, %8 " CTL      \
+               "\n\tv_mov_b32_dpp %6, %8 " CTL "\n\tv_mov_b32_dpp %7, %8 " CTL                                       \
+               : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)       \
+               : "v"(b));
+    if constexpr (OP == 28) { REP16(BODYX("v_bitop3_b32", "bitop3:0xde")) }
+    if constexpr (OP == 29) { REP16(BODY("v_or3_b32")) }
+    if constexpr (OP == 30) { REP16(BODY("v_and_or_b32")) }
+    if constexpr (OP == 31) { REP16(BODYDPP("wave_shr:1 row_mask:0xf bank_mask:0xf")) }
+    if constexpr (OP == 32) { REP16(BODY("v_lshl_or_b32")) }
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * 4 + (threadIdx.x >> 6)] = t1 - t0;
@@ -119,5 +136,10 @@ int main() {
   run<8>("v_min_i32", cus);
   run<10>("v_med3_i32", cus);
   run<11>("v_pk_sub_u16", cus);
+  run<28>("v_bitop3_b32", cus);
+  run<29>("v_or3_b32", cus);
+  run<30>("v_and_or_b32", cus);
+  run<31>("v_mov_b32_dpp wave_shr:1", cus);
+  run<32>("v_lshl_or_b32", cus);
   return 0;
 }
