@@ -79,7 +79,8 @@ typedef struct nwk_stats {
   int32_t fill_launches;     /* fill-kernel launches in the call */
   int32_t device_finalized;  /* batches whose pairs were finalized on the device */
   int32_t linear_space_pairs; /* pairs aligned with the linear-space traceback */
-  int32_t reserved[2];
+  int32_t window_retries;    /* nw_align_bits windowed storage: pairs re-run with full storage (path left the window) */
+  int32_t reserved[1];
 } nwk_stats;
 
 /* Defaults for nwk_opts (device 0, auto everything). */

@@ -34,7 +34,10 @@
 // 16-byte stores thus writes 1 KB contiguous across the wave (whole lines:
 // a lane-major 64-byte-stride layout wrote partial lines at ~1.1 TB/s).  A
 // band has 64 * sblocks steps (sblocks = nchunks + 32: the last row runs 2047
-// columns behind the first).
+// columns behind the first).  Windowed storage (PairDesc::bits_w > 0) keeps
+// only bits_nblk blocks per band, from block bits_blk_lo(band) on: the band's
+// steps within bits_w columns of the diagonal j = i n / m; a traceback that
+// leaves them flags the pair for a full-storage re-run (FillArgs::retry).
 #include "nwk_internal.h"
 
 namespace nwk {
@@ -80,7 +83,7 @@ __device__ __noinline__ u64 bits_wait(const u64* p, bool mine, unsigned epoch, u
 template <int NP, int SR, bool MASK, bool PROD>
 __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsigned x1, unsigned yp0, unsigned yp1,
                                            unsigned w0, unsigned w1, unsigned (&H)[NP], unsigned (&V)[NP],
-                                           const unsigned* cons, unsigned* ring, unsigned* st) {
+                                           const unsigned* cons, unsigned* ring, unsigned* st, bool sto) {
   unsigned dw[8], uw[8];
   // the band-above entries are read one step ahead (an LDS read's latency
   // would otherwise sit on every step's dependence chain)
@@ -151,6 +154,7 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
   if (dw[0] == 0x9e3779b9u && uw[7] == 0x7f4a7c15u) *st = dw[1] ^ uw[2];
   return;
 #endif
+  if (!sto) return;  // block outside the pair's stored window (PairDesc::bits_w)
   __builtin_nontemporal_store(u4{dw[0], dw[1], dw[2], dw[3]}, reinterpret_cast<u4*>(st));
   __builtin_nontemporal_store(u4{dw[4], dw[5], dw[6], dw[7]}, reinterpret_cast<u4*>(st + 256));
   __builtin_nontemporal_store(u4{uw[0], uw[1], uw[2], uw[3]}, reinterpret_cast<u4*>(st + 512));
@@ -167,7 +171,8 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
 
 __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd, unsigned char* obuf, int lane,
                                            unsigned* prog) {
-  const int64_t bdw = (int64_t)pd.sblocks * 8192;
+  const int nblk = pd.bits_nblk, win = pd.bits_w;
+  const int64_t bdw = (int64_t)nblk * 1024;  // dwords per band
   const unsigned* mat = a.mat + pd.mat_off;
   uint8_t* ops = a.ops + pd.ops_off;
   const unsigned ob = (unsigned)(uintptr_t)obuf;
@@ -185,9 +190,9 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
   // position: band b, band row r (0..2047, -1 = the row above the band), column c (0-based)
   int b = (pd.m - 1) / kBR, r = (pd.m - 1) % kBR, c = pd.n - 1;
   if (a.dbg_notrace) c = -1;  // NWK_NOTRACE (fill timing): no moves, the walk "ends" at (m, n)
-  int tb = -1, ts = 0, tt = 0;
+  int tb = -1, ts = 0, tt = 0, blo = 0, slo = 0;
   unsigned vd0 = 0, vu0 = 0, vd1 = 0, vu1 = 0;
-  bool bad = false;
+  bool bad = false, out = false;
   while (c >= 0 && (b > 0 || r >= 0)) {
     if (r < 0) {  // into the band above
       --b;
@@ -195,16 +200,25 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
     }
     int t = r >> 5;
     int s = c + r;
+    if (b != tb) {
+      blo = bits_blk_lo(b, pd.m, pd.n, win);
+      slo = 8 * blo;  // lowest stored step of band b
+    }
+    if ((unsigned)((s >> 3) - blo) >= (unsigned)nblk) {  // the path left the stored window
+      out = true;
+      break;
+    }
     BITS_PROG(0x50000000u | ((unsigned)(Lc & 0xfff) << 16) | ((unsigned)(r & 0xff) << 8) | (unsigned)(c & 0xff));
     if (b != tb || s > ts || s <= ts - 64 || (t != tt && t != tt - 1)) {
       tb = b;
       ts = s;
       tt = t;
       const int sl = s - lane;
+      const int rel = (sl >> 3) - blo;
       vd0 = vu0 = vd1 = vu1 = 0;
-      if (sl >= 0) {
+      if (sl >= 0 && (unsigned)rel < (unsigned)nblk) {
         const unsigned* p0 =
-            mat + (int64_t)b * bdw + (int64_t)(sl >> 3) * 1024 + ((sl & 7) >> 2) * 256 + t * 4 + (sl & 3);
+            mat + (int64_t)b * bdw + (int64_t)rel * 1024 + ((sl & 7) >> 2) * 256 + t * 4 + (sl & 3);
         vd0 = __builtin_nontemporal_load(p0);
         vu0 = __builtin_nontemporal_load(p0 + 512);
         if (t > 0) {
@@ -242,7 +256,7 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
       if (Lc - flushed >= 192) flush(Lc & ~3);
       if (c < 0 || r < 0) break;
       t = r >> 5;
-      if (s <= ts - 64 || (t != tt && t != tt - 1)) break;
+      if (s <= ts - 64 || (t != tt && t != tt - 1) || s < slo) break;
     }
     if (Lc > pd.m + pd.n) {
       bad = true;
@@ -253,9 +267,11 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
   flush(Lc);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0) {
-    a.oplen[pd.slot] = Lc;
+    // out of the window: a placeholder result (no moves) and the re-run flag
+    a.oplen[pd.slot] = out ? 0 : Lc;
     // the walk ends on the border: row b * 2048 + r + 1, column c + 1
-    a.endij[pd.slot] = a.dbg_notrace ? make_int2(pd.m, pd.n) : make_int2(b * kBR + r + 1, c + 1);
+    a.endij[pd.slot] = (a.dbg_notrace || out) ? make_int2(pd.m, pd.n) : make_int2(b * kBR + r + 1, c + 1);
+    if (out) a.retry[pd.slot] = 1;
   }
 }
 
@@ -304,7 +320,8 @@ __global__ __launch_bounds__(256) void nw_align_bits(FillArgs a) {
     const int nch = pd.nchunks, nsb = pd.sblocks;
     const u64* gin = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)(from_above ? band - 1 : 0) * nch * NG;
     u64* gout = a.bnd + pd.bnd_off + (int64_t)band * nch * NG;
-    unsigned* mb = a.mat + pd.mat_off + (int64_t)band * nsb * 8192 + lane * 4;
+    const int nblk = pd.bits_nblk, blo = bits_blk_lo(band, pd.m, pd.n, pd.bits_w);
+    unsigned* mb = a.mat + pd.mat_off + (int64_t)band * nblk * 1024 + lane * 4;
     // y windows: lane t's window for the half starting at step s_h is position s_h - 32 t
     const unsigned* ywp = a.yw + 2 * (pd.e_off - 32 * (int64_t)lane);
     unsigned yp0 = 0, yp1 = 0;
@@ -350,13 +367,15 @@ __global__ __launch_bounds__(256) void nw_align_bits(FillArgs a) {
       for (int blk = 0; blk < 8; ++blk) {
         const int s0 = 64 * sb + 8 * blk;
         const unsigned w0 = blk < 4 ? wa0 : wb0, w1 = blk < 4 ? wa1 : wb1;
-        unsigned* st = mb + (int64_t)(s0 >> 3) * 1024;
+        const int rel = (s0 >> 3) - blo;
+        const bool sto = (unsigned)rel < (unsigned)nblk;
+        unsigned* st = mb + (int64_t)rel * 1024;
         if (mask) {
-          if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st);
-          else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st);
+          if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto);
+          else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto);
         } else {
-          if (prod) bits_block<NP, SR, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st);
-          else bits_block<NP, SR, false, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st);
+          if (prod) bits_block<NP, SR, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto);
+          else bits_block<NP, SR, false, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto);
         }
         if ((blk & 3) == 3) {  // end of a 32-step half: its window becomes the previous one
           yp0 = w0;

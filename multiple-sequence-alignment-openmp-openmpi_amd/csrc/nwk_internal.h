@@ -54,7 +54,18 @@ struct PairDesc {
   // linear-space traceback group (FillArgs.lin_mode 2): bands in the group,
   // trace start cell, row where the trace stops (the group's top)
   int32_t lin_nb, lin_i, lin_j, lin_stop;
+  // kBits windowed storage: only the 8-step blocks within bits_w columns of
+  // the pair's diagonal j = i n / m are stored (bits_w = 0: every block);
+  // bits_nblk blocks per band (band b keeps blocks bits_blk_lo(b) ..)
+  int32_t bits_w, bits_nblk;
 };
+
+// kBits: first stored 8-step block of band b (see PairDesc::bits_w)
+__host__ __device__ inline int bits_blk_lo(int b, int m, int n, int w) {
+  if (w <= 0) return 0;
+  const int64_t lo = (int64_t)b * kBitsRows * n / m - w;
+  return lo <= 0 ? 0 : (int)(lo >> 3);
+}
 
 struct FillArgs {
   const PairDesc* pairs;
@@ -91,6 +102,7 @@ struct FillArgs {
   const int* prow;         // kProfileDP: per X column (DP row) 8 ints {rc[0..5], gx, H[i][0]} at pairs[].x_off
   const int* pcol;         // kProfileDP: per Y column (DP column) 8 ints {cnt[0..5], gy, H[0][j]} at pairs[].y_off
   const unsigned* yw;      // kBits: per y position p two dwords (code bit planes of y[p .. p+31], y[p] at bit 31), at pairs[].e_off
+  int* retry;              // kBits windowed storage: per slot, 1 = the path left the stored window (re-run in full)
 };
 constexpr int kProfSyms = 6;  // kProfileDP: symbols + gap per column profile
 

@@ -131,6 +131,8 @@ struct PairWork {
   int spec;                       // segmented traceback: spec_every
   int nguess;                     // segmented traceback: start columns per speculative boundary
   int64_t njobs;                  // queued extra guesses (spec boundaries x (nguess - 1))
+  int bits_w = 0;                 // kBits windowed storage: half-width in columns (0 = full), see PairDesc
+  int bits_nblk = 0;              // kBits: stored 8-step blocks per band
 };
 
 }  // namespace
@@ -165,7 +167,7 @@ struct nwk_ctx {
   // batch buffers
   DevBuf d_work;                // matrices | boundary granules | op strings
   int64_t clean_b = 0;          // leading bytes of d_work holding only zeros / old-epoch granules
-  DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij, d_done, d_stamps, d_prog;
+  DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij, d_done, d_stamps, d_prog, d_retry;
   DevBuf d_segctl;              // kPacked2: task-done flags | segment info | traceback records
   DevBuf d_pen, d_hash;         // device finalize (nw_hash): per pair penalty, problemhash
   DevBuf d_msa[3];              // nwk_msa: row profiles | column profiles | granules, matrices, moves
@@ -173,6 +175,7 @@ struct nwk_ctx {
   bool has_us = false;          // some input byte is '_': trims need the host finalize
   HostBuf h_tasks;
   HostBuf h_pairs[2], h_oplen[2], h_endij[2], h_ops[2];  // double-buffered: batch b+1 runs while b finalizes
+  HostBuf h_retry;  // kBits windowed storage: per slot of the last batch, 1 = re-run with full storage
 
   nwk_stats stats{};
 };
@@ -202,7 +205,8 @@ void nwk_ctx_destroy(nwk_ctx* c) {
   c->d_yw.release();
   c->d_work.release();
   c->d_pairs.release(); c->d_tasks.release(); c->d_ctl.release();
-  c->d_oplen.release(); c->d_endij.release(); c->d_done.release(); c->d_stamps.release();
+  c->d_oplen.release(); c->d_endij.release(); c->d_done.release(); c->d_stamps.release(); c->d_retry.release();
+  c->h_retry.release();
   c->d_segctl.release(); c->d_prog.release(); c->d_pen.release(); c->d_hash.release();
   for (auto& b : c->d_msa) b.release();
   for (int b = 0; b < 2; ++b) { c->h_pen[b].release(); c->h_hash[b].release(); }
@@ -499,12 +503,22 @@ void seg_footprint(PairWork* w, int mode, int E, int NG) {
 inline int bits_sblocks(int64_t nch) { return (int)(nch + 32); }
 constexpr int kBitsGranPerChunk = 8;
 
+// kBits stored blocks per band: every block, or (bits_w > 0) the blocks of
+// steps r + j with |j - i n / m| <= bits_w over the band's 2048 rows i
+int64_t bits_nblk_of(int m, int n, int w) {
+  const int64_t all = 8 * (int64_t)bits_sblocks(ceil_div(n, 64));
+  if (w <= 0) return all;
+  const int64_t width = (kBitsRows - 1) + ceil_div((int64_t)(kBitsRows - 1) * n, m) + 2 * (int64_t)w + 16;
+  return std::min(all, ceil_div(width, 8) + 1);
+}
+
 void footprint(PairWork* w, int bits, int mode, bool affine) {
   if (mode == kBits) {
     const int64_t nb = ceil_div(w->m, kBitsRows), nch = ceil_div(w->n, 64);
     w->segops_b = w->segctl_b = 0;
     w->spec = 0;
-    w->mat_dw = nb * bits_sblocks(nch) * 8192;
+    w->bits_nblk = (int)bits_nblk_of(w->m, w->n, w->bits_w);
+    w->mat_dw = nb * w->bits_nblk * 1024;
     w->bnd_gr = (nb - 1) * nch * kBitsGranPerChunk;
     w->ops_b = round_up((int64_t)w->m + w->n, 16);
     return;
@@ -854,8 +868,11 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   HIP_TRY(hipSetDevice(c->device));
 
   // Degenerate pairs (m == 0 or n == 0) have no DP cells: prefix only.
+  // (capacity for one full-storage re-run of every pair: a kBits windowed pair
+  // whose path leaves its window is appended once, and the async finalize
+  // holds pointers into dp, so it must never reallocate)
   std::vector<PairWork> dp;
-  dp.reserve(work.size());
+  dp.reserve(2 * work.size());
   for (auto& w : work) {
     st.cells += (double)w.m * (double)w.n;
     if (w.m == 0 || w.n == 0) {
@@ -877,6 +894,40 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     if ((pl.mode == kPacked || band_pairs(pl.mode)) &&
         (rc = build_sel(c, pl.K0 < 0 ? 1 : 0, band_pairs(pl.mode) ? 64 : 1)) != NWK_OK)
       return rc;
+  }
+  // kBits windowed storage.  When the job's full 2-bit matrices exceed the
+  // workspace, store only the steps within W columns of each pair's diagonal
+  // j = i n / m, W the widest candidate that fits the job in one batch (at
+  // least 1024).  Paths of random C3 pairs stay within ~1.2k columns of it
+  // (tools/pathdev.py); a path that leaves its window is detected by the
+  // traceback and the pair re-runs with full storage (the retry list below),
+  // so results never depend on W.  NWK_BITS_WIN: 0 off, W > 0 forced.
+  static const int win_env = getenv("NWK_BITS_WIN") ? atoi(getenv("NWK_BITS_WIN")) : -1;
+  if (pl.mode == kBits && !dp.empty() && win_env != 0) {
+    auto total_b = [&]() {
+      int64_t mat = 0, bnd = 0, ops = 0;
+      for (const auto& w : dp) mat += w.mat_dw, bnd += w.bnd_gr, ops += w.ops_b;
+      return mat * 4 + bnd * 8 + 3 * ops + 8192;
+    };
+    auto set_w = [&](int W) {
+      for (auto& w : dp) {
+        w.bits_w = W;
+        footprint(&w, pl.bits, pl.mode, sc.affine);
+      }
+    };
+    int W = win_env > 0 ? win_env : 0;
+    if (W == 0 && total_b() > c->budget) {
+      static const int cand[] = {8192, 6144, 4096, 3072, 2560, 2048, 1536, 1024};
+      for (int wc : cand) {
+        set_w(wc);
+        if (total_b() <= c->budget) {
+          W = wc;
+          break;
+        }
+      }
+      if (W == 0) W = 1024;
+    }
+    set_w(W);
   }
   // Largest first (LPT inside the device; longest bands dequeued first).
   // kPacked2 (NWK_SORT != 0): by traceback length m + n first, so the pairs
@@ -1048,6 +1099,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       d.nbands = (int)ceil_div(w.m, pl.mode == kBits ? kBitsRows : kBandRows);
       d.nchunks = (int)ceil_div(w.n, 64);
       d.sblocks = pl.mode == kBits ? bits_sblocks(d.nchunks) : sblocks_of(pl.mode, d.nchunks);
+      d.bits_w = w.bits_w;
+      d.bits_nblk = w.bits_nblk;
       d.slot = q;
       d.spec_every = w.spec;
       d.nguess = w.nguess;
@@ -1100,6 +1153,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     if ((rc = c->d_oplen.ensure(sizeof(int) * np)) != NWK_OK) return rc;
     if ((rc = c->d_endij.ensure(sizeof(int2) * np)) != NWK_OK) return rc;
     if ((rc = c->d_done.ensure(sizeof(unsigned) * np)) != NWK_OK) return rc;
+    if ((rc = c->d_retry.ensure(sizeof(int) * np)) != NWK_OK) return rc;
+    if ((rc = c->h_retry.ensure(sizeof(int) * np)) != NWK_OK) return rc;
     if ((rc = c->h_oplen[par].ensure(sizeof(int) * np)) != NWK_OK) return rc;
     if ((rc = c->h_endij[par].ensure(sizeof(int2) * np)) != NWK_OK) return rc;
     if ((rc = c->h_ops[par].ensure((size_t)ops)) != NWK_OK) return rc;
@@ -1107,6 +1162,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipMemcpyAsync(c->d_tasks.p, tk, sizeof(int2) * ntasks, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(c->d_ctl.p, 0, 256, c->stream));
     HIP_TRY(hipMemsetAsync(c->d_done.p, 0, sizeof(unsigned) * np, c->stream));
+    bool windowed = false;
+    for (int q = 0; q < np && !windowed; ++q) windowed = pd[q].bits_w > 0;
+    if (windowed) HIP_TRY(hipMemsetAsync(c->d_retry.p, 0, sizeof(int) * np, c->stream));
     // [tdone u32 | seginfo 8 x int | recs u64 | job ready u32 | head, tail | jobs int2]
     const int64_t seginfo_base_b = ntasks * 4;
     const int64_t rec_base_b = round_up(seginfo_base_b + nsegs * 32, 8);
@@ -1142,6 +1200,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.lin_mode = 0;
     fa.prog = nullptr;
     fa.yw = pl.mode == kBits ? c->d_yw.as<unsigned>() : nullptr;
+    fa.retry = c->d_retry.as<int>();
     if (getenv("NWK_WATCHDOG")) {
       if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;
       HIP_TRY(hipMemsetAsync(c->d_prog.p, 0, 4 * (size_t)(grid + 1) * 4, c->stream));
@@ -1231,6 +1290,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipMemcpyAsync(&herr, fa.err, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_oplen[par].p, fa.oplen, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_endij[par].p, fa.endij, sizeof(int2) * np, hipMemcpyDeviceToHost, c->stream));
+    if (windowed) HIP_TRY(hipMemcpyAsync(c->h_retry.p, fa.retry, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
     if (devhash) {  // 68 bytes per pair instead of the move strings
       if ((rc = c->h_pen[par].ensure(4 * (size_t)np)) != NWK_OK) return rc;
       if ((rc = c->h_hash[par].ensure(64 * (size_t)np)) != NWK_OK) return rc;
@@ -1333,6 +1393,22 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     st.matrix_bytes += mat * 4;
     st.batches += 1;
     st.fill_launches += 1;
+    // kBits windowed storage: pairs whose path left the window get no result
+    // from this batch; they re-run with full storage in a later batch
+    std::vector<char> skip;
+    if (windowed) {
+      const int* rt = c->h_retry.as<int>();
+      for (int q = 0; q < np; ++q) {
+        if (!rt[q]) continue;
+        if (skip.empty()) skip.assign((size_t)np, 0);
+        skip[q] = 1;
+        PairWork w = dp[pos + q];
+        w.bits_w = 0;
+        footprint(&w, pl.bits, pl.mode, sc.affine);
+        dp.push_back(w);  // capacity reserved: no reallocation
+        st.window_retries += 1;
+      }
+    }
     // ---- host finalize, overlapped with the next batch's kernel: it runs on
     // its own thread over this batch's host buffer set while the loop goes
     // on to set up, launch and wait for batch b+1 (buffer set par ^ 1).
@@ -1345,13 +1421,17 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     const PairWork* dw = dp.data() + pos;
     const int* hpen = c->h_pen[par].as<int>();
     const uint8_t* hhash = c->h_hash[par].as<uint8_t>();
-    auto job = [c, a1, a2, np, dw, pd, ol, ej, hops, ops_base_b, sc, penalties, hashes, chain, devhash, hpen, hhash]() {
+    auto job = [c, a1, a2, np, dw, pd, ol, ej, hops, ops_base_b, sc, penalties, hashes, chain, devhash, hpen, hhash,
+                skip]() {
+      auto skipped = [&](int64_t q) { return !skip.empty() && skip[(size_t)q]; };
       if (devhash) {
         for (int64_t q = 0; q < np; ++q) {
+          if (skipped(q)) continue;
           penalties[dw[q].out] = hpen[q];
           memcpy(hashes + 64 * dw[q].out, hhash + 64 * q, 64);
         }
       } else parallel_for(a1 ? 1 : c->host_threads, np, [&](int64_t q) {
+        if (skipped(q)) return;
         const PairWork& w = dw[q];
         const PairDesc& d = pd[q];
         Finalized f;
@@ -1361,7 +1441,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         memcpy(hashes + 64 * w.out, f.hash, 64);
       });
       if (chain) {  // serial: jobs never overlap each other (fin.join() before the next starts)
-        for (int64_t q = 0; q < np; ++q) chain->ready[dw[q].out] = 1;
+        for (int64_t q = 0; q < np; ++q)
+          if (!skipped(q)) chain->ready[dw[q].out] = 1;
         chain->advance();
       }
     };

@@ -49,7 +49,8 @@ class Stats(ctypes.Structure):
                 ("matrix_bytes", ctypes.c_int64), ("batches", ctypes.c_int32),
                 ("bits", ctypes.c_int32), ("mode", ctypes.c_int32),
                 ("fill_launches", ctypes.c_int32), ("device_finalized", ctypes.c_int32),
-                ("linear_space_pairs", ctypes.c_int32), ("reserved", ctypes.c_int32 * 2)]
+                ("linear_space_pairs", ctypes.c_int32), ("window_retries", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 # Every exported symbol of include/nwk.h with its ctypes signature.

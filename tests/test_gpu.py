@@ -126,17 +126,30 @@ import numpy as np
 sys.path.insert(0, sys.argv[1])
 import seqalign
 genes = [bytes.fromhex(g) for g in json.loads(sys.stdin.read())]
+ws = int(sys.argv[2]) if len(sys.argv) > 2 else 64 << 20
 k = len(genes)
 out = []
 for pxy, pgap in ((3, 2), (5, 1)):
-    with seqalign.Engine(device=0, workspace_bytes=64 << 20) as e:
+    with seqalign.Engine(device=0, workspace_bytes=ws) as e:
         e.set_sequences(genes)
         pen, hs = e.align_pairs(np.arange(k * (k - 1) // 2, dtype=np.int64), pxy, pgap)
         st = e.stats()
-    out.append({"mode": st["mode"], "batches": st["batches"], "pen": [int(v) for v in pen],
-                "hs": [x.tobytes().hex() for x in hs]})
+    out.append({"mode": st["mode"], "batches": st["batches"], "retries": st["window_retries"],
+                "pen": [int(v) for v in pen], "hs": [x.tobytes().hex() for x in hs]})
 print(json.dumps(out))
 """
+
+
+def _run_child(genes, env_extra, ws=64 << 20):
+    import json
+    import sys
+
+    env = dict(os.environ, **env_extra)
+    res = subprocess.run([sys.executable, "-c", _ORDER_SCRIPT, os.path.dirname(seqalign.__file__), str(ws)],
+                         input=json.dumps([g.hex() for g in genes]).encode(), env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
+    assert res.returncode == 0, res.stderr.decode()[-2000:]
+    return json.loads(res.stdout.decode().strip().splitlines()[-1])
 
 
 @pytest.mark.parametrize("order", ["0", "1", "3"])
@@ -147,23 +160,39 @@ def test_bits_kernel_task_orders_multi_batch(order):
     with a small workspace, so several batches reuse the granule region.  The
     order is read once per process, hence the child process.  Bit-exact vs the
     oracle on 3/2 and 5/1 (the reference's two penalty sets)."""
-    import json
-    import subprocess
-    import sys
-
     r = random.Random(77)
     genes = _rand_genes(r, 7, 5000, 7000, ACGT)
-    env = dict(os.environ, NWK_ORDER=order)
-    res = subprocess.run([sys.executable, "-c", _ORDER_SCRIPT, os.path.dirname(seqalign.__file__)],
-                         input=json.dumps([g.hex() for g in genes]).encode(), env=env,
-                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
-    assert res.returncode == 0, res.stderr.decode()[-2000:]
-    out = json.loads(res.stdout.decode().strip().splitlines()[-1])
+    out = _run_child(genes, {"NWK_ORDER": order, "NWK_BITS_WIN": "0"})
     for (pxy, pgap), o in zip(((3, 2), (5, 1)), out):
         assert o["mode"] == 8 and o["batches"] > 1
         _, opens, ohs = oracle.all_pairs(genes, pxy, pgap)
         assert o["pen"] == opens
         assert o["hs"] == ohs
+
+
+@pytest.mark.parametrize("win", ["auto", "48", "700", "3000"])
+def test_bits_windowed_storage_and_full_rerun(win):
+    """nw_align_bits windowed storage (only steps within W columns of each
+    pair's diagonal are stored; nwk_runtime.cpp): a path that leaves the
+    window is caught by the traceback and the pair re-runs with full storage
+    (window_retries).  Ragged pairs (slopes far from 1), mutated copies and
+    multi-band lengths, with a workspace too small for full storage (so the
+    automatic window engages); results bit-exact vs the oracle for any W."""
+    r = random.Random(4242)
+    genes = [bytes(r.choice(ACGT) for _ in range(L)) for L in (700, 2500, 4100, 6000)]
+    genes += _mutants(r, bytes(r.choice(ACGT) for _ in range(5000)), 3, ACGT)
+    # swapped halves: the optimal path runs ~3500 columns off the diagonal
+    P, Q = (bytes(r.choice(ACGT) for _ in range(3500)) for _ in range(2))
+    genes += [P + Q, Q + P]
+    env = {} if win == "auto" else {"NWK_BITS_WIN": win}
+    out = _run_child(genes, env, ws=24 << 20)
+    for (pxy, pgap), o in zip(((3, 2), (5, 1)), out):
+        assert o["mode"] == 8
+        _, opens, ohs = oracle.all_pairs(genes, pxy, pgap)
+        assert o["pen"] == opens
+        assert o["hs"] == ohs
+        if win == "48":
+            assert o["retries"] > 0, "a 48-column window must send some pairs to the full re-run"
 
 
 def test_subset_and_order_of_pair_ids(engine):
