@@ -10,7 +10,8 @@
 //     v(i,j) = D - U,    h(i,j) = D - L.
 // Borders are all zero.  The reference's traceback (skel:229-262: DIAG on a
 // match, DIAG if H_diag + pxy == H, UP if H_up + pgap == H, else LEFT) needs
-// two bits per cell: diag = match | (D == S_mismatch) and up = (v == 0).
+// two bits per cell: diag = match | (D == S_mismatch), and plane 0 of v
+// (stored raw: UP is v == 0).
 //
 // Bit slicing.  A value x in [0, NP], NP = 2 pgap, is held as NP thermometer
 // planes t_k = [x > k].  Then max is OR, and D - U is the convolution
@@ -73,6 +74,60 @@ __device__ __noinline__ u64 bits_wait(const u64* p, bool mine, unsigned epoch, u
   }
 }
 
+// The plane update with explicit v_bitop3_b32 (any 3-input boolean function,
+// full rate on gfx950: 2.7 cycles per wave-instruction against 4.4 for
+// v_or3 / v_and_or, profiles/r02/valu_probe_gfx950.txt).  Truth-table
+// immediates are built from the operand masks kA = S0, kB = S1, kC = S2.
+#ifndef NWK_BITS_BOP3
+#define NWK_BITS_BOP3 1
+#endif
+constexpr unsigned kA = 0xF0u, kB = 0xCCu, kC = 0xAAu;
+#define BOP3(a, b, c, f) __builtin_amdgcn_bitop3_b32((a), (b), (c), (unsigned)((f) & 0xFFu))
+
+// acc | OR_{j >= J, j + K < NP} (~X_j & D_{j+K});  D_i is all ones for i < SR
+template <int NP, int SR, int K, int J>
+__device__ __forceinline__ unsigned bits_conv(unsigned acc, const unsigned (&X)[NP], const unsigned (&D)[NP]) {
+  if constexpr (J + K >= NP) {
+    return acc;
+  } else {
+    if constexpr (J + K < SR) acc = BOP3(acc, X[J], X[J], kA | ~kB);
+    else acc = BOP3(acc, X[J], D[J + K], kA | (~kB & kC));
+    return bits_conv<NP, SR, K, J + 1>(acc, X, D);
+  }
+}
+
+// plane K of the difference D - X:  OR_j (~X_j & D_{j+K})
+template <int NP, int SR, int K>
+__device__ __forceinline__ unsigned bits_diff(const unsigned (&X)[NP], const unsigned (&D)[NP]) {
+  constexpr bool ones0 = K < SR;  // D_K all ones
+  if constexpr (K + 1 >= NP) {
+    if constexpr (ones0) return ~X[0];
+    else return BOP3(X[0], D[K], D[K], ~kA & kB);
+  } else {
+    constexpr bool ones1 = K + 1 < SR;
+    unsigned acc;
+    if constexpr (ones0 && ones1) {
+      acc = BOP3(X[0], X[1], X[1], ~kA | ~kB);
+    } else if constexpr (ones0) {
+      acc = BOP3(X[0], X[1], D[K + 1], ~kA | (~kB & kC));
+    } else {
+      acc = BOP3(X[0], D[K], D[K], ~kA & kB);
+      acc = BOP3(acc, X[1], D[K + 1], kA | (~kB & kC));
+    }
+    return bits_conv<NP, SR, K, 2>(acc, X, D);
+  }
+}
+
+template <int NP, int SR>
+__device__ __forceinline__ void bits_diffs(const unsigned (&X)[NP], const unsigned (&D)[NP], unsigned (&out)[NP]) {
+  out[0] = bits_diff<NP, SR, 0>(X, D);
+  out[1] = bits_diff<NP, SR, 1>(X, D);
+  if constexpr (NP == 4) {
+    out[2] = bits_diff<NP, SR, 2>(X, D);
+    out[3] = bits_diff<NP, SR, 3>(X, D);
+  }
+}
+
 // Eight steps s0 .. s0+7 (s0 % 8 == 0) of one band.
 //   x0, x1   code bit planes of this lane's 32 rows
 //   yp, w    y windows: previous half and this 32-step half (bit 31 - q of w =
@@ -108,6 +163,28 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
     const unsigned sh = 31u - (unsigned)(s & 31);
     const unsigned y0 = __builtin_amdgcn_alignbit(yp0, w0, sh);
     const unsigned y1 = __builtin_amdgcn_alignbit(yp1, w1, sh);
+#if NWK_BITS_BOP3
+    const unsigned match = BOP3(x0 ^ y0, x1, y1, ~(kA | (kB ^ kC)));  // ~((x0^y0) | (x1^y1))
+    unsigned U[NP], D[NP], Vn[NP], Hn[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      // lane t-1's plane word (lane 0: the band above), its bit 31 enters at bit 0
+      const unsigned T = (unsigned)__builtin_amdgcn_update_dpp((int)inj[k], (int)H[k], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
+      U[k] = __builtin_amdgcn_alignbit(H[k], T, 31);
+      D[k] = k < SR ? ~0u : BOP3(match, U[k], V[k], kA | kB | kC);
+    }
+    bits_diffs<NP, SR>(U, D, Vn);
+    bits_diffs<NP, SR>(V, D, Hn);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      V[k] = Vn[k];
+      H[k] = Hn[k];
+    }
+    if constexpr (SR < 0) dw[q] = match;
+    else if constexpr (SR >= NP) dw[q] = ~0u;
+    else dw[q] = BOP3(match, D[SR], D[SR], kA | ~kB);  // match | ~D_SR
+    uw[q] = V[0];  // stored raw: the traceback's UP test is v == 0 (bit clear)
+#else
     const unsigned mism = (x0 ^ y0) | (x1 ^ y1);
     const unsigned match = ~mism;
     unsigned nU[NP], nV[NP], D[NP];
@@ -134,7 +211,8 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
     if constexpr (SR < 0) dw[q] = match;
     else if constexpr (SR >= NP) dw[q] = ~0u;
     else dw[q] = match | ~D[SR];
-    uw[q] = ~V[0];
+    uw[q] = V[0];
+#endif
     if constexpr (MASK) {  // columns < 0 keep v = 0 (the left border seen by column 0)
       const int e = s - 32 * lane;
       const unsigned M = e >= 31 ? ~0u : (e < 0 ? 0u : (2u << e) - 1u);
@@ -242,7 +320,7 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
         --r;
         --c;
         s -= 2;
-      } else if ((u >> bit) & 1u) {
+      } else if (!((u >> bit) & 1u)) {  // up: v == 0 (the stored word is v's plane 0)
         op = 'U';
         --r;
         s -= 1;
