@@ -1121,16 +1121,17 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     // Pair-major (pairs already largest first): a pair's bands are dequeued
     // together, so pairs finish one after another and each one's traceback
     // runs concurrently with the fill of the pairs after it.
-    // nw_align_bits with several rounds of tasks per wave slot: band-major.  Its
-    // bands trail each other by 2048 + 64 steps, so bands of one pair dequeued
-    // together wait b x 2112 steps; band-major spaces them by a whole round of
-    // other pairs' bands (C3: 11.5k -> 14.0k GCUPS; big13, one round: pair-major
-    // 6.0k vs 5.5k).  NWK_ORDER overrides (0 pair-major, 1 band-major, g >= 2
-    // groups of g pairs, band-major inside).
+    // nw_align_bits with more than one round of tasks per wave slot: band-major.
+    // Its bands trail each other by 2048 + 64 steps, so bands of one pair
+    // dequeued together wait b x 2112 steps; band-major spaces them by a round
+    // of other pairs' bands (C3: 11.5k -> 14.0k GCUPS; C3's 8-rank shard, 1.5
+    // rounds: 59 -> 51 ms; big13, under one round: pair-major 40 vs 44 ms).
+    // NWK_ORDER overrides (0 pair-major, 1 band-major, g >= 2 groups of g
+    // pairs, band-major inside).
     int64_t t = 0;
     static const int order_env = getenv("NWK_ORDER") ? atoi(getenv("NWK_ORDER")) : -1;
     int order = order_env;
-    if (order < 0) order = pl.mode == kBits && ntasks > 2 * 4 * (int64_t)grid ? 1 : 0;
+    if (order < 0) order = pl.mode == kBits && ntasks > 4 * (int64_t)grid ? 1 : 0;
     if (order == 1) {  // band-major (experiment)
       for (int b = 0; b < maxb; ++b)
         for (int q = 0; q < np; ++q)
