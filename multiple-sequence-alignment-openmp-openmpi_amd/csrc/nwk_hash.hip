@@ -7,7 +7,7 @@
 //   sha512 = sw::sha512::calculate (sha512.hh:159-164, FIPS 180-4).
 //
 // nw_rows materialises align1 / align2 of every pair in HBM (coalesced,
-// scan-based, one workgroup per pair) and sums the path cost (= dp[m][n], the
+// wave-scan based, one workgroup per pair) and sums the path cost (= dp[m][n], the
 // reference's penalty); nw_hash then runs one lane per row over 16-byte loads
 // (SHA-512 is sequential within a message), and the two digests meet through
 // a lane shuffle so the even lane can hash their 256 hex characters.  Valid when no input byte is
@@ -85,13 +85,26 @@ __device__ __forceinline__ uint64_t hex16(uint32_t v) {  // 8 nibbles of v -> 8 
 
 }  // namespace
 
-// Rows + penalty, one workgroup per pair: the moves are split into 256
-// contiguous chunks, a block scan gives each chunk its first x / y index, and
-// every thread writes its chunk of align1 / align2 (skel:263-272 prefix, then
-// the traced moves in forward order).
+// Rows + penalty, one workgroup per pair (skel:263-272 prefix, then the traced
+// moves in forward order).  Wave w of the four owns a contiguous quarter of the
+// forward moves.  Pass 1 counts the quarter's x / y advances; pass 2 walks it
+// 64 moves per iteration, lane l taking move base + l: one coalesced 64-byte
+// read of the (reversed) move string, a wave scan of the packed advances
+// {x | y << 16} for each lane's x / y index, coalesced 64-byte row writes.
+// (The first version gave each of 256 threads a private ~400-move chunk read
+// byte by byte: every load touched 256 lines, 7 ms on C3.)
+__device__ __forceinline__ unsigned wave_incl_scan(unsigned v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned u = (unsigned)__shfl_up((int)v, o);
+    v += lane >= o ? u : 0u;
+  }
+  return v;
+}
+
 __global__ __launch_bounds__(256) void nw_rows(HashArgs h) {
-  __shared__ int sx[256], sy[256];
-  __shared__ long long sp[256];
+  __shared__ int tx[4], ty[4];
+  __shared__ long long sp[4];
   const int q = blockIdx.x;
   const PairDesc pd = h.pairs[q];
   const int nops = h.oplen[pd.slot];
@@ -102,50 +115,59 @@ __global__ __launch_bounds__(256) void nw_rows(HashArgs h) {
   const uint8_t* y = h.raw + pd.y_off;
   uint8_t* r1 = h.rows1 + (pd.ops_off - h.ops_base);
   uint8_t* r2 = h.rows2 + (pd.ops_off - h.ops_base);
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int t = tid; t < pre; t += 256) {  // prefix run
     r1[t] = e.x > 0 ? x[t] : (uint8_t)'_';
     r2[t] = e.x > 0 ? (uint8_t)'_' : y[t];
   }
-  const int C = (nops + 255) / 256;
-  const int f0 = min(nops, tid * C), f1 = min(nops, f0 + C);  // forward move index f: op = ops[nops-1-f]
-  int dx = 0, dy = 0;
-  for (int f = f0; f < f1; ++f) {
+  const int Q = ((nops + 3) / 4 + 63) & ~63;  // moves per wave, whole iterations
+  const int F0 = min(nops, w * Q), F1 = min(nops, F0 + Q);
+  // pass 1: this quarter's advances
+  int cx = 0, cy = 0;
+  for (int f = F0 + lane; f < F1; f += 64) {
     const unsigned op = ops[nops - 1 - f];
     const bool d = op == 'D', up = op == 'U' || op == 'u';
-    dx += (d || up) ? 1 : 0;
-    dy += (d || !up) ? 1 : 0;
+    cx += (d || up) ? 1 : 0;
+    cy += (d || !up) ? 1 : 0;
   }
-  sx[tid] = dx;
-  sy[tid] = dy;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cx += __shfl_xor(cx, o);
+    cy += __shfl_xor(cy, o);
+  }
+  if (lane == 0) { tx[w] = cx; ty[w] = cy; }
   __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {  // inclusive scan
-    const int vx = tid >= o ? sx[tid - o] : 0, vy = tid >= o ? sy[tid - o] : 0;
-    __syncthreads();
-    sx[tid] += vx;
-    sy[tid] += vy;
-    __syncthreads();
-  }
-  int ix = e.x + sx[tid] - dx, iy = e.y + sy[tid] - dy;
+  int ix = e.x, iy = e.y;
+  for (int v = 0; v < w; ++v) { ix += tx[v]; iy += ty[v]; }
+  // pass 2
   long long pen = 0;
-  for (int f = f0; f < f1; ++f) {
-    const unsigned op = ops[nops - 1 - f];
+  for (int base = F0; base < F1; base += 64) {
+    const int f = base + lane;
+    const bool live = f < F1;
+    const unsigned op = live ? ops[nops - 1 - f] : 0u;
     const bool d = op == 'D', up = op == 'U' || op == 'u';
-    const unsigned cx = (d || up) ? x[ix] : (unsigned)'_';
-    const unsigned cy = (d || !up) ? y[iy] : (unsigned)'_';
-    r1[pre + f] = (uint8_t)cx;
-    r2[pre + f] = (uint8_t)cy;
-    pen += d ? (cx == cy ? 0 : h.pxy) : (op == 'u' || op == 'l' ? h.gopen : h.gext);
-    ix += (d || up) ? 1 : 0;
-    iy += (d || !up) ? 1 : 0;
+    const bool ax = live && (d || up), ay = live && (d || !up);
+    const unsigned adv = (ax ? 1u : 0u) | (ay ? 0x10000u : 0u);
+    const unsigned inc = wave_incl_scan(adv, lane);
+    const unsigned exc = inc - adv;
+    if (live) {
+      const unsigned chx = ax ? x[ix + (int)(exc & 0xffffu)] : (unsigned)'_';
+      const unsigned chy = ay ? y[iy + (int)(exc >> 16)] : (unsigned)'_';
+      r1[pre + f] = (uint8_t)chx;
+      r2[pre + f] = (uint8_t)chy;
+      pen += d ? (chx == chy ? 0 : h.pxy) : (op == 'u' || op == 'l' ? h.gopen : h.gext);
+    }
+    const unsigned tot = (unsigned)__shfl((int)inc, 63);
+    ix += (int)(tot & 0xffffu);
+    iy += (int)(tot >> 16);
   }
-  sp[tid] = pen;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) pen += __shfl_xor(pen, o);
+  if (lane == 0) sp[w] = pen;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) sp[tid] += sp[tid + o];
-    __syncthreads();
-  }
-  if (tid == 0) h.penalties[pd.slot] = (int)(sp[0] + (pre > 0 ? h.gopen + (long long)(pre - 1) * h.gext : 0));
+  if (tid == 0)
+    h.penalties[pd.slot] =
+        (int)(sp[0] + sp[1] + sp[2] + sp[3] + (pre > 0 ? h.gopen + (long long)(pre - 1) * h.gext : 0));
 }
 
 // SHA-512 of one materialised row per lane (lane 2q: align1 of pair q, lane
