@@ -41,7 +41,33 @@ __constant__ uint64_t kK512[80] = {
     0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
     0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
 
-__device__ __forceinline__ uint64_t rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit helpers on the 32-bit halves: a rotate by a constant is two
+// v_alignbit_b32 (a generic 64-bit rotate compiled to two 64-bit shifts and two
+// ORs), and every 3-input boolean function (XOR3, Ch, Maj) is one
+// v_bitop3_b32 per half (truth tables over S0 = 0xF0, S1 = 0xCC, S2 = 0xAA).
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));  // {lo, hi}: a 64-bit value's halves in one register pair
+template <int N>
+__device__ __forceinline__ uint64_t rotr(uint64_t x) {
+  const u32x2 v = __builtin_bit_cast(u32x2, x);
+  u32x2 r;
+  if constexpr (N < 32) {
+    r.x = __builtin_amdgcn_alignbit(v.y, v.x, N);
+    r.y = __builtin_amdgcn_alignbit(v.x, v.y, N);
+  } else {
+    r.x = __builtin_amdgcn_alignbit(v.x, v.y, N - 32);
+    r.y = __builtin_amdgcn_alignbit(v.y, v.x, N - 32);
+  }
+  return __builtin_bit_cast(uint64_t, r);
+}
+template <unsigned F>
+__device__ __forceinline__ uint64_t bop3(uint64_t a, uint64_t b, uint64_t c) {
+  const u32x2 x = __builtin_bit_cast(u32x2, a), y = __builtin_bit_cast(u32x2, b), z = __builtin_bit_cast(u32x2, c);
+  u32x2 r;
+  r.x = __builtin_amdgcn_bitop3_b32(x.x, y.x, z.x, F);
+  r.y = __builtin_amdgcn_bitop3_b32(x.y, y.y, z.y, F);
+  return __builtin_bit_cast(uint64_t, r);
+}
+constexpr unsigned kXor3 = 0x96u, kCh = 0xCAu, kMaj = 0xE8u;
 
 struct Sha {
   uint64_t s[8];
@@ -60,13 +86,13 @@ struct Sha {
         wt = w[t];
       } else {
         const uint64_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-        const uint64_t s0 = rotr(w15, 1) ^ rotr(w15, 8) ^ (w15 >> 7);
-        const uint64_t s1 = rotr(w2, 19) ^ rotr(w2, 61) ^ (w2 >> 6);
+        const uint64_t s0 = bop3<kXor3>(rotr<1>(w15), rotr<8>(w15), w15 >> 7);
+        const uint64_t s1 = bop3<kXor3>(rotr<19>(w2), rotr<61>(w2), w2 >> 6);
         wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
         w[t & 15] = wt;
       }
-      const uint64_t t1 = h + (rotr(e, 14) ^ rotr(e, 18) ^ rotr(e, 41)) + ((e & f) ^ (~e & g)) + kK512[t] + wt;
-      const uint64_t t2 = (rotr(a, 28) ^ rotr(a, 34) ^ rotr(a, 39)) + ((a & b) ^ (a & c) ^ (b & c));
+      const uint64_t t1 = h + bop3<kXor3>(rotr<14>(e), rotr<18>(e), rotr<41>(e)) + bop3<kCh>(e, f, g) + kK512[t] + wt;
+      const uint64_t t2 = bop3<kXor3>(rotr<28>(a), rotr<34>(a), rotr<39>(a)) + bop3<kMaj>(a, b, c);
       h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
     }
     s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
