@@ -54,9 +54,11 @@ struct PairDesc {
   // linear-space traceback group (FillArgs.lin_mode 2): bands in the group,
   // trace start cell, row where the trace stops (the group's top)
   int32_t lin_nb, lin_i, lin_j, lin_stop;
-  // kBits windowed storage: only the 8-step blocks within bits_w columns of
-  // the pair's diagonal j = i n / m are stored (bits_w = 0: every block);
-  // bits_nblk blocks per band (band b keeps blocks bits_blk_lo(b) ..)
+  // Windowed storage (kBits, kAffinePk): only the steps within bits_w columns
+  // of the pair's diagonal j = i n / m are stored (bits_w = 0: all of them).
+  // kBits: bits_nblk 8-step blocks per band (band b keeps blocks
+  // bits_blk_lo(b) ..); kAffinePk: bits_nblk 64-step super-blocks per band
+  // pair (band pair p keeps super-blocks pka_sb_lo(p) ..).
   int32_t bits_w, bits_nblk;
 };
 
@@ -65,6 +67,15 @@ __host__ __device__ inline int bits_blk_lo(int b, int m, int n, int w) {
   if (w <= 0) return 0;
   const int64_t lo = (int64_t)b * kBitsRows * n / m - w;
   return lo <= 0 ? 0 : (int)(lo >> 3);
+}
+
+// kAffinePk: first stored super-block of band pair p.  Its rows R+1 .. R+1024
+// (R = 1024 p) put cell (i, j) of half h, lane t at step j - 1 + t + 64 h, so
+// the window's cells j >= i n / m - w sit at steps >= R n / m - w - 1.
+__host__ __device__ inline int pka_sb_lo(int p, int m, int n, int w) {
+  if (w <= 0) return 0;
+  const int64_t lo = (int64_t)p * 2 * kBandRows * n / m - w - 64;
+  return lo <= 0 ? 0 : (int)(lo >> 6);
 }
 
 struct FillArgs {
@@ -102,7 +113,7 @@ struct FillArgs {
   const int* prow;         // kProfileDP: per X column (DP row) 8 ints {rc[0..5], gx, H[i][0]} at pairs[].x_off
   const int* pcol;         // kProfileDP: per Y column (DP column) 8 ints {cnt[0..5], gy, H[0][j]} at pairs[].y_off
   const unsigned* yw;      // kBits: per y position p two dwords (code bit planes of y[p .. p+31], y[p] at bit 31), at pairs[].e_off
-  int* retry;              // kBits windowed storage: per slot, 1 = the path left the stored window (re-run in full)
+  int* retry;              // windowed storage: per slot, 1 = the path left the stored window (re-run in full)
 };
 constexpr int kProfSyms = 6;  // kProfileDP: symbols + gap per column profile
 

@@ -1796,8 +1796,10 @@ __device__ __forceinline__ unsigned pk_or(unsigned a, unsigned m) { return a | m
 //   F7:     row 7's F' of the previous step (lane t+1's row-0 F-up, publish)
 //   bH, bF: LDS rings of the band-above H and F' rows (scaled, low 16 bits)
 //   hb0:    packed border H of row 0 (masked steps), + r * ge4 for row r
-template <bool MASK>
-__device__ __forceinline__ void step_block_pka(int s0, int lane, unsigned (&Hc)[kRows], unsigned (&Ec)[kRows],
+//   STO:    code stores: 1 always, 0 never (outside the stored window,
+//           PairDesc::bits_w), 2 when `sto` (the masked super-blocks)
+template <bool MASK, int STO>
+__device__ __forceinline__ void step_block_pka(int s0, int lane, bool sto, unsigned (&Hc)[kRows], unsigned (&Ec)[kRows],
                                                unsigned (&Nb)[kRows], unsigned& F7, unsigned& U, unsigned& stH,
                                                unsigned& stF, const unsigned (&pl)[kRows], const unsigned (&ph)[kRows],
                                                const unsigned* srow, const int* bH, const int* bF, unsigned upsel,
@@ -1861,15 +1863,17 @@ __device__ __forceinline__ void step_block_pka(int s0, int lane, unsigned (&Hc)[
       }
     }
     F7 = fup;
-    if (k & 1) {
+    if (STO == 1 || (STO == 2 && sto)) {
+      if (k & 1) {
 #pragma unroll
-      for (int r = 0; r < kRows; ++r) {
-        const unsigned X = __builtin_amdgcn_perm(Nn[r], Nb[r], 0x06040200u);
-        if ((k & 3) == 1) {
-          Xa[r] = X;
-        } else {
-          const unsigned D = (Xa[r] & 0x0f0f0f0fu) | ((X << 4) & 0xf0f0f0f0u);
-          __builtin_nontemporal_store(D, mptr + ((k >> 2) * kRows + r) * kWave);
+        for (int r = 0; r < kRows; ++r) {
+          const unsigned X = __builtin_amdgcn_perm(Nn[r], Nb[r], 0x06040200u);
+          if ((k & 3) == 1) {
+            Xa[r] = X;
+          } else {
+            const unsigned D = (Xa[r] & 0x0f0f0f0fu) | ((X << 4) & 0xf0f0f0f0u);
+            __builtin_nontemporal_store(D, mptr + ((k >> 2) * kRows + r) * kWave);
+          }
         }
       }
     }
@@ -1891,15 +1895,21 @@ __device__ __forceinline__ void trace_pair_pka(const FillArgs& a, const PairDesc
   using C = TbConf<4, 2>;
   using Y = Lay<4, 2>;
   constexpr int SPC = Y::SPC, RPC = Y::RPC;
-  const int64_t bdw = band_dwords(4, pd.sblocks);
-  const int ncols = 64 * pd.sblocks / SPC;
+  // windowed storage (PairDesc::bits_w): band pair p holds super-blocks
+  // pka_sb_lo(p) .. + nsb - 1; a cell outside them reads as code 16, which
+  // ends the walk and flags the pair for a full-storage re-run
+  const int nsb = pd.bits_w > 0 ? pd.bits_nblk : pd.sblocks;
+  const int64_t bdw = band_dwords(4, nsb);
+  const int ncols = 64 * nsb / SPC;
   const unsigned* mb = a.mat + pd.mat_off;
   const int lane_off = (lane >> 4) * kWave + (lane & 15);
+  auto sblo_of = [&](int b) { return pka_sb_lo(b >> 1, pd.m, pd.n, pd.bits_w); };
   auto issue = [&](int b, int q, int t0) {
     const unsigned* src = mb + Y::base(b, bdw) + t0 + lane_off;
+    const int c0 = 16 * sblo_of(b);
 #pragma unroll
     for (int k = 0; k < C::TILE / 64; ++k) {
-      int c = C::TC * q - C::OV + k / (RPC / 4);
+      int c = C::TC * q - C::OV + k / (RPC / 4) - c0;
       c = c < 0 ? 0 : (c >= ncols ? ncols - 1 : c);
       __builtin_amdgcn_global_load_lds((gbl_void*)(src + (int64_t)c * (RPC * kWave) + 4 * (k % (RPC / 4)) * kWave),
                                        (lds_void*)&L.tile[0][64 * k], 4, 0, 0);
@@ -1907,9 +1917,9 @@ __device__ __forceinline__ void trace_pair_pka(const FillArgs& a, const PairDesc
   };
   auto drain = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
   uint8_t* ops = a.ops + pd.ops_off;
-  int i = pd.m, j = pd.n, Lc = 0, flushed = 0, tb = -1, tq = 0, tt0 = 0;
+  int i = pd.m, j = pd.n, Lc = 0, flushed = 0, tb = -1, tq = 0, tt0 = 0, tsb = 0;
   unsigned st = 0;  // 0 = H, 1 = F, 2 = E
-  bool bad = false;
+  bool bad = false, out = false;
   const unsigned ob = lds_addr(&L.obuf[0]);
   auto flush = [&](int upto) {
     const int from = flushed & ~3;
@@ -1939,6 +1949,7 @@ __device__ __forceinline__ void trace_pair_pka(const FillArgs& a, const PairDesc
         issue(b, q, nt0);
         drain();
         tb = b; tq = q; tt0 = nt0;
+        tsb = sblo_of(b);
       }
     }
     // this lane's cell (ci, cj) = (i - li, j - lj)
@@ -1951,18 +1962,33 @@ __device__ __forceinline__ void trace_pair_pka(const FillArgs& a, const PairDesc
       const int slo = C::TS * tq - C::OV * SPC, shi = C::TS * tq + C::TS;
       const int cbase = C::TC * tq - C::OV;
       if (ww >= 0 && tt >= tt0 && tt < tt0 + C::TL && ss >= slo && ss < shi) {
-        const unsigned ad = lds_addr(&L.tile[0][0]) + 4u * (unsigned)(((ss / SPC - cbase) * RPC + rr) * C::TL + (tt - tt0));
-        unsigned v;
-        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ad) : "memory");
-        code = (v >> Y::shift(ss, rr, hh)) & 15u;
+        if ((unsigned)((ss >> 6) - tsb) < (unsigned)nsb) {
+          const unsigned ad = lds_addr(&L.tile[0][0]) + 4u * (unsigned)(((ss / SPC - cbase) * RPC + rr) * C::TL + (tt - tt0));
+          unsigned v;
+          asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ad) : "memory");
+          code = (v >> Y::shift(ss, rr, hh)) & 15u;
+        } else {
+          code = 16u;
+        }
       } else {
-        code = getG_global<4, 2>(a.mat, pd, bdw, ci, cj);
+        const int w1 = ci - 1, b1 = w1 / kBandRows, wr = w1 - b1 * kBandRows, t1 = wr / kRows, r1 = wr - t1 * kRows;
+        const int h1 = Y::hb(b1), s1 = Y::step(t1, r1, cj, h1), sl = sblo_of(b1);
+        if ((unsigned)((s1 >> 6) - sl) < (unsigned)nsb) {
+          const unsigned d = mb[Y::base(b1, bdw) + ((int64_t)(s1 / SPC - 16 * sl) * RPC + r1) * kWave + t1];
+          code = (d >> Y::shift(s1, r1, h1)) & 15u;
+        } else {
+          code = 16u;
+        }
       }
     }
     // scalar walk through the block
     int di = 0, dj = 0;
     for (;;) {
       const unsigned c = __builtin_amdgcn_readlane(code, di * 8 + dj);
+      if (c & 16u) {  // the path left the stored window
+        out = true;
+        break;
+      }
       unsigned op = 0;
       if (st == 0) {
         const unsigned src = c & 3u;
@@ -1995,6 +2021,7 @@ __device__ __forceinline__ void trace_pair_pka(const FillArgs& a, const PairDesc
     }
     i -= di;
     j -= dj;
+    if (out) break;
     if (Lc - flushed >= 160) flush(Lc & ~3);
     if (bad || Lc > pd.m + pd.n) {
       if (lane == 0) atomicOr(a.err, 16u);
@@ -2005,8 +2032,10 @@ __device__ __forceinline__ void trace_pair_pka(const FillArgs& a, const PairDesc
   flush(Lc);
   drain();
   if (lane == 0) {
-    a.oplen[pd.slot] = Lc;
-    a.endij[pd.slot] = make_int2(i, j);
+    // out of the window: a placeholder result (no moves) and the re-run flag
+    a.oplen[pd.slot] = out ? 0 : Lc;
+    a.endij[pd.slot] = out ? make_int2(pd.m, pd.n) : make_int2(i, j);
+    if (out) a.retry[pd.slot] = 1;
   }
 }
 
@@ -2064,7 +2093,10 @@ __global__ __launch_bounds__(256) void nw_align_pka(FillArgs a) {
     const int last_chunk = pd.nchunks > 0 ? pd.nchunks - 1 : 0;
     u64* goutH = a.bnd + pd.bnd_off + (int64_t)bp * bstride + lane;
     u64* goutF = goutH + fbase;
-    unsigned* mptr = a.mat + pd.mat_off + (int64_t)bp * 2 * band_dwords(W, pd.sblocks) + lane;
+    // windowed storage: this band pair keeps super-blocks sblo .. sblo + nsb - 1
+    const int nsb = pd.bits_w > 0 ? pd.bits_nblk : pd.sblocks;
+    const int sblo = pka_sb_lo(bp, pd.m, pd.n, pd.bits_w);
+    unsigned* mptr = a.mat + pd.mat_off + (int64_t)bp * 2 * band_dwords(W, nsb) + lane;
 
     // bases: H(first row of the half, column 0) = go + (row + 1) ge, so the
     // border of lane t's row r is kPkaBias + 4 (8t + r) ge in both halves
@@ -2145,18 +2177,28 @@ __global__ __launch_bounds__(256) void nw_align_pka(FillArgs a) {
       const unsigned xfer = lane == 0 ? (unsigned)(4 * (base_lo - base_hi)) << 16 : 0u;
       u64* gpH = goutH + 64 * (sb >= 2 ? sb - 2 : 0);
       u64* gpF = goutF + 64 * (sb >= 2 ? sb - 2 : 0);
+      const bool sto = (unsigned)(sb - sblo) < (unsigned)nsb;
       for (int blk = 0; blk < 8; ++blk) {
         const int s0 = sb * 64 + blk * 8;
         const unsigned* srow = w + blk * 8 + 64 - lane;
         const bool pub = pub_sb && blk == 7;
         if (sb < 2)
-          step_block_pka<true>(s0, lane, Hc, Ec, Nb, F7, U, stH, stF, pl, ph, srow, slH + blk * 8, slF + blk * 8, upsel,
-                               mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0, xfer);
+          step_block_pka<true, 2>(s0, lane, sto, Hc, Ec, Nb, F7, U, stH, stF, pl, ph, srow, slH + blk * 8,
+                                  slF + blk * 8, upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0, xfer);
+        else if (sto)
+          step_block_pka<false, 1>(s0, lane, sto, Hc, Ec, Nb, F7, U, stH, stF, pl, ph, srow, slH + blk * 8,
+                                   slF + blk * 8, upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0, xfer);
         else
-          step_block_pka<false>(s0, lane, Hc, Ec, Nb, F7, U, stH, stF, pl, ph, srow, slH + blk * 8, slF + blk * 8,
-                                upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0, xfer);
-        mptr += 2 * kRows * kWave;
-        wait_vm_keep4<kBlockStores>(sw0, sw1, pH, pF);
+          step_block_pka<false, 0>(s0, lane, sto, Hc, Ec, Nb, F7, U, stH, stF, pl, ph, srow, slH + blk * 8,
+                                   slF + blk * 8, upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0, xfer);
+        // the counted wait keeps this block's stores in flight; a block that
+        // stored nothing waits for the prefetches themselves
+        if (sto) {
+          mptr += 2 * kRows * kWave;
+          wait_vm_keep4<kBlockStores>(sw0, sw1, pH, pF);
+        } else {
+          wait_vm_keep4<0>(sw0, sw1, pH, pF);
+        }
       }
       __builtin_amdgcn_wave_barrier();
     }

@@ -512,6 +512,15 @@ int64_t bits_nblk_of(int m, int n, int w) {
   return std::min(all, ceil_div(width, 8) + 1);
 }
 
+// kAffinePk stored super-blocks per band pair (bits_w > 0): pka_sb_lo(p) lies
+// at or below the steps of its rows' window cells (>= R n / m - w - 1) and the
+// highest is below (R + 1024) n / m + w + 127 (lane 63, the odd band's skew)
+int64_t pka_nsb_of(int m, int n, int w) {
+  const int64_t all = sblocks_of(kAffinePk, ceil_div(n, 64));
+  if (w <= 0) return all;
+  return std::min(all, ceil_div(ceil_div((int64_t)2 * kBandRows * n, m) + 2 * (int64_t)w + 256, 64) + 2);
+}
+
 void footprint(PairWork* w, int bits, int mode, bool affine) {
   if (mode == kBits) {
     const int64_t nb = ceil_div(w->m, kBitsRows), nch = ceil_div(w->n, 64);
@@ -529,7 +538,12 @@ void footprint(PairWork* w, int bits, int mode, bool affine) {
   w->segops_b = w->segctl_b = 0;
   w->spec = 0;
   if (segmented(mode)) seg_footprint(w, mode, 0, 1);
-  w->mat_dw = (band_pairs(mode) ? 2 * nt : nb) * band_dwords(bits, sblocks_of(mode, nch));
+  if (mode == kAffinePk && w->bits_w > 0) {
+    w->bits_nblk = (int)pka_nsb_of(w->m, w->n, w->bits_w);
+    w->mat_dw = 2 * nt * band_dwords(bits, w->bits_nblk);
+  } else {
+    w->mat_dw = (band_pairs(mode) ? 2 * nt : nb) * band_dwords(bits, sblocks_of(mode, nch));
+  }
   w->bnd_gr = (nt - 1) * nch * 64 * (affine ? 2 : 1);  // affine: H and F boundary rows
   w->ops_b = round_up((int64_t)w->m + w->n, 16);
 }
@@ -902,8 +916,18 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   // (tools/pathdev.py); a path that leaves its window is detected by the
   // traceback and the pair re-runs with full storage (the retry list below),
   // so results never depend on W.  NWK_BITS_WIN: 0 off, W > 0 forced.
+  //
+  // kAffinePk (nw_align_pka) the same way, per 64-step super-block of a band
+  // pair.  Its bands need many rounds of tasks per wave slot to run free of
+  // the band-pair chains (a band pair dequeued right behind the one above
+  // waits on it), which only a window gives at C5's size (full storage: 13
+  // pairs per batch).  Affine paths stray further (C5 pairs: up to ~4.6k
+  // columns, profiles/r02/pathdev_c5.txt), so it keeps W = 8192 and takes
+  // more batches (C5: 4 of ~124 pairs, ~12 rounds of wave slots each).
   static const int win_env = getenv("NWK_BITS_WIN") ? atoi(getenv("NWK_BITS_WIN")) : -1;
-  if (pl.mode == kBits && !dp.empty() && win_env != 0) {
+  static const int winb_env = getenv("NWK_WIN_BATCHES") ? atoi(getenv("NWK_WIN_BATCHES")) : 0;
+  if ((pl.mode == kBits || pl.mode == kAffinePk) && !dp.empty() && win_env != 0) {
+    const int64_t nbat = winb_env > 0 ? winb_env : pl.mode == kAffinePk ? (int64_t)1 << 30 : 1;
     auto total_b = [&]() {
       int64_t mat = 0, bnd = 0, ops = 0;
       for (const auto& w : dp) mat += w.mat_dw, bnd += w.bnd_gr, ops += w.ops_b;
@@ -920,7 +944,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       static const int cand[] = {8192, 6144, 4096, 3072, 2560, 2048, 1536, 1024};
       for (int wc : cand) {
         set_w(wc);
-        if (total_b() <= c->budget) {
+        if (total_b() <= nbat * c->budget) {
           W = wc;
           break;
         }
@@ -1131,7 +1155,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     int64_t t = 0;
     static const int order_env = getenv("NWK_ORDER") ? atoi(getenv("NWK_ORDER")) : -1;
     int order = order_env;
-    if (order < 0) order = pl.mode == kBits && ntasks > 4 * (int64_t)grid ? 1 : 0;
+    if (order < 0) order = (pl.mode == kBits || pl.mode == kAffinePk) && ntasks > 4 * (int64_t)grid ? 1 : 0;
     if (order == 1) {  // band-major (experiment)
       for (int b = 0; b < maxb; ++b)
         for (int q = 0; q < np; ++q)
@@ -1459,9 +1483,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fprintf(stderr, "nwk host: setup+launch %.3f ms, kernel+copies wait %.3f ms, finalize join %.3f ms, last finalize %.3f ms\n", h_setup, h_sync, h_join, h_last);
   c->stats = st;
   if (c->opts.verbose)
-    fprintf(stderr, "nwk: %zu pairs, %.3g cells, fill %.3f ms (%.1f GCUPS), traceback %.3f ms, total %.3f ms, bits %d mode %d, %d batch(es)\n",
+    fprintf(stderr, "nwk: %zu pairs, %.3g cells, fill %.3f ms (%.1f GCUPS), traceback %.3f ms, total %.3f ms, bits %d mode %d, %d batch(es), window %d, %d retries\n",
             work.size(), st.cells, st.fill_ms, st.fill_ms > 0 ? st.cells / st.fill_ms / 1e6 : 0.0,
-            st.traceback_ms, st.total_ms, st.bits, st.mode, st.batches);
+            st.traceback_ms, st.total_ms, st.bits, st.mode, st.batches, dp.empty() ? 0 : dp[0].bits_w, (int)st.window_retries);
   return NWK_OK;
 }
 

@@ -195,6 +195,56 @@ def test_bits_windowed_storage_and_full_rerun(win):
             assert o["retries"] > 0, "a 48-column window must send some pairs to the full re-run"
 
 
+_AFF_WIN_SCRIPT = r"""
+import json, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import seqalign
+genes = [bytes.fromhex(g) for g in json.loads(sys.stdin.read())]
+k = len(genes)
+out = []
+for pxy, go, ge in ((3, 3, 1), (4, 2, 2)):
+    with seqalign.Engine(device=0, workspace_bytes=int(sys.argv[2])) as e:
+        e.set_sequences(genes)
+        pen, hs = e.align_pairs_affine(np.arange(k * (k - 1) // 2, dtype=np.int64), pxy, go, ge)
+        st = e.stats()
+    out.append({"mode": st["mode"], "batches": st["batches"], "retries": st["window_retries"],
+                "pen": [int(v) for v in pen], "hs": [x.tobytes().hex() for x in hs]})
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("win", ["auto", "40", "600", "2000"])
+def test_affine_packed_windowed_storage_and_full_rerun(win):
+    """nw_align_pka windowed storage: band pair p stores only the 64-step
+    super-blocks pka_sb_lo(p) .. + nsb - 1 around the diagonal (nwk_internal.h);
+    a traceback that leaves them flags the pair and it re-runs with full
+    storage.  Ragged lengths (multi band-pair, slopes far from 1), mutated
+    copies and swapped halves (paths ~3000 columns off the diagonal), with a
+    workspace too small for full storage; bit-exact vs the oracle for any W."""
+    import json
+    import sys
+
+    r = random.Random(5151)
+    genes = [bytes(r.choice(ACGT) for _ in range(L)) for L in (900, 2600, 4100, 5200)]
+    genes += _mutants(r, bytes(r.choice(ACGT) for _ in range(4500)), 2, ACGT)
+    P, Q = (bytes(r.choice(ACGT) for _ in range(3000)) for _ in range(2))
+    genes += [P + Q, Q + P]
+    env = dict(os.environ, **({} if win == "auto" else {"NWK_BITS_WIN": win}))
+    res = subprocess.run([sys.executable, "-c", _AFF_WIN_SCRIPT, os.path.dirname(seqalign.__file__), str(40 << 20)],
+                         input=json.dumps([g.hex() for g in genes]).encode(), env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
+    assert res.returncode == 0, res.stderr.decode()[-2000:]
+    out = json.loads(res.stdout.decode().strip().splitlines()[-1])
+    for (pxy, go, ge), o in zip(((3, 3, 1), (4, 2, 2)), out):
+        assert o["mode"] == 7, "nw_align_pka expected"
+        _, opens, ohs = oracle.all_pairs_affine(genes, pxy, go, ge)
+        assert o["pen"] == opens
+        assert o["hs"] == ohs
+        if win == "40":
+            assert o["retries"] > 0, "a 40-column window must send some pairs to the full re-run"
+
+
 def test_subset_and_order_of_pair_ids(engine):
     r = random.Random(5)
     genes = _rand_genes(r, 7, 50, 900, ACGT)

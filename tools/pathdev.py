@@ -1,9 +1,13 @@
 """Path deviation from the proportional diagonal for workload pairs (GPU).
 For pair (i, j): max over the alignment of |col - row * n / m| (row = x index).
+Affine workloads (c5) trace with their (go, ge).
 usage: python tools/pathdev.py [workload=c3] [npairs=16]"""
+import math
 import sys
+
 sys.path.insert(0, "multiple-sequence-alignment-openmp-openmpi_amd")
-import seqalign, workloads
+import seqalign, workloads  # noqa: E402
+
 wl = sys.argv[1] if len(sys.argv) > 1 else "c3"
 npairs = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 desc, k, L, pxy, pgap, affine = workloads.SYNTH[wl]
@@ -11,14 +15,13 @@ genes = workloads.synth(k, L)
 with seqalign.Engine(device=0) as e:
     devs = []
     for p in range(npairs):
-        i, j = seqalign.pair_of(p) if hasattr(seqalign, "pair_of") else (None, None)
-        if i is None:
-            import math
-            i = int((1 + math.isqrt(1 + 8 * p)) // 2)
-            j = p - i * (i - 1) // 2
+        i = int((1 + math.isqrt(1 + 8 * p)) // 2)
+        j = p - i * (i - 1) // 2
         x, y = genes[i], genes[j]
-        r = e.get_minimum_penalty(x, y, pxy, pgap)
-        pen, a1, a2 = r if isinstance(r, tuple) else (r, None, None)
+        if affine:
+            pen, a1, a2 = e.get_minimum_penalty_affine(x, y, pxy, affine[0], affine[1])
+        else:
+            pen, a1, a2 = e.get_minimum_penalty(x, y, pxy, pgap)
         m, n = len(x), len(y)
         row = col = 0
         worst = 0
