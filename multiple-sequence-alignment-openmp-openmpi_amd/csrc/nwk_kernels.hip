@@ -2039,7 +2039,16 @@ __device__ __forceinline__ void trace_pair_pka(const FillArgs& a, const PairDesc
   }
 }
 
-__global__ __launch_bounds__(256) void nw_align_pka(FillArgs a) {
+// NWK_PKA_WPE > 0: at least that many waves per SIMD (A/B builds)
+#ifndef NWK_PKA_WPE
+#define NWK_PKA_WPE 0
+#endif
+#if NWK_PKA_WPE > 0
+#define NWK_PKA_OCC __attribute__((amdgpu_waves_per_eu(NWK_PKA_WPE)))
+#else
+#define NWK_PKA_OCC
+#endif
+__global__ __launch_bounds__(256) NWK_PKA_OCC void nw_align_pka(FillArgs a) {
   constexpr int W = 4;
   __shared__ __attribute__((aligned(16))) int ringH_all[4][128];
   __shared__ __attribute__((aligned(16))) int ringF_all[4][128];
