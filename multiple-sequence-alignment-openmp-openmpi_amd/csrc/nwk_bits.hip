@@ -247,6 +247,13 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
     if (prog && lane == 0) __hip_atomic_store((gu32*)prog, (unsigned)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
   } while (0)
 
+// NWK_TRACE_MASKS 1: a branch-free walk on per-row ballot masks (SGPR bit tests)
+// instead of two v_readlane per move.  Measured equal (C3 8-rank shard: 9.7-10.0
+// vs 9.5 ms per 100k-move trace: a lone wave issues about one instruction per
+// 4 cycles, so ~50 instructions per move bound either walk), so 0 stays.
+#ifndef NWK_TRACE_MASKS
+#define NWK_TRACE_MASKS 0
+#endif
 __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd, unsigned char* obuf, int lane,
                                            unsigned* prog) {
   const int nblk = pd.bits_nblk, win = pd.bits_w;
@@ -306,6 +313,43 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
       }
     }
     // walk inside the tile
+#if NWK_TRACE_MASKS
+    // Row masks: bit l of Dr / Ur = the diag / up bit of row r at step ts - l
+    // (one ballot each).  Every D or U move goes to row r - 1, so its masks
+    // are built one move ahead and the decisions are scalar bit tests on
+    // SGPRs; only the ballots (off the decision chain) and the move's LDS
+    // write touch the VALU.
+    auto row_masks = [&](int x, u64& dm, u64& um) {
+      const bool h = (x >> 5) == tt;
+      const unsigned sh = (unsigned)(x & 31);
+      dm = __builtin_amdgcn_ballot_w64((((h ? vd0 : vd1) >> sh) & 1u) != 0u);
+      um = __builtin_amdgcn_ballot_w64((((h ? vu0 : vu1) >> sh) & 1u) != 0u);
+    };
+    u64 Dr, Ur, Dn, Un;
+    row_masks(r, Dr, Ur);
+    row_masks(r - 1, Dn, Un);  // (rows outside the tile: junk, never read -- the walk leaves first)
+    int L = ts - s;
+    const int rlo = 32 * (tt - 1);  // lowest row of the tile
+    for (;;) {
+      // branch-free move: D (diag bit), else U (up bit clear), else L
+      const unsigned isD = (unsigned)(Dr >> L) & 1u;
+      const unsigned isU = ~isD & ~(unsigned)(Ur >> L) & 1u;
+      const unsigned down = isD | isU;  // row r - 1 next
+      const unsigned op = isD ? 'D' : isU ? 'U' : 'L';
+      asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(op) : "memory");
+      ++Lc;
+      r -= (int)down;
+      c -= (int)(isD | (down ^ 1u));
+      L += 1 + (int)isD;
+      Dr = down ? Dn : Dr;
+      Ur = down ? Un : Ur;
+      if (Lc - flushed >= 192) flush(Lc & ~3);
+      if ((c | r) < 0 || L >= 64 || r < rlo || ts - L < slo) break;
+      row_masks(r - 1, Dn, Un);
+    }
+    t = r >> 5;
+    s = ts - L;
+#else
     for (;;) {
       // straight-line uniform code: one select per word, one v_readlane each
       const int L = __builtin_amdgcn_readfirstlane(ts - s);
@@ -336,6 +380,7 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
       t = r >> 5;
       if (s <= ts - 64 || (t != tt && t != tt - 1) || s < slo) break;
     }
+#endif
     if (Lc > pd.m + pd.n) {
       bad = true;
       break;
@@ -375,6 +420,8 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
   unsigned* cons = cons_all[wid];
   unsigned* ring = ring_all[wid];
   constexpr int NG = 2 * NP;  // granules per 64-column chunk
+  // verbose >= 2 timeline (FillArgs::stamps, layout in nwk_runtime.cpp)
+  if (a.stamps && threadIdx.x == 0) atomicMin(a.stamps + 11 * a.ntasks_pairs, (u64)__builtin_amdgcn_s_memrealtime());
 
   for (;;) {
     unsigned tk = 0;
@@ -419,13 +466,22 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
     u64 g = 0;
     if (from_above && gl) g = __hip_atomic_load((gu64*)(gin + lane), BITS_RLX);
     bool ok = true;
+    const u64 t_task = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+    u64 cyc_wait = 0, cyc_wait0 = 0, n_wait = 0;
 
     for (int sb = 0; sb < nsb; ++sb) {
       BITS_PROG(0x20000000u | (unsigned)sb);
       // --- band-above row for columns 64 sb .. 64 sb + 63 -> cons
       if (from_above && sb < nch) {
         if (!__all(!gl || (unsigned)(g >> 32) == a.epoch)) {
+          const u64 tw = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
           g = bits_wait(gin + (int64_t)sb * NG + lane, gl, a.epoch, g, a.err);
+          if (a.stamps) {
+            const u64 d = __builtin_amdgcn_s_memtime() - tw;
+            cyc_wait += d;
+            if (sb == 0) cyc_wait0 = d;
+            ++n_wait;
+          }
           if (!__all(!gl || (unsigned)(g >> 32) == a.epoch)) { ok = false; break; }
         }
         const unsigned dat = (unsigned)g;
@@ -490,6 +546,13 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
     }
     BITS_PROG(0x30000000u);
     if (!ok) return;
+    if (a.stamps && lane == 0) {  // per pair: band cycles, of which waiting on the band above
+      atomicAdd(a.stamps + 8 * pd.slot + 6, (u64)(__builtin_amdgcn_s_memtime() - t_task));
+      atomicAdd(a.stamps + 8 * pd.slot + 7, cyc_wait);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot, cyc_wait0);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 1, n_wait);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 2, (u64)nsb);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -502,7 +565,9 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
       // (NWK_NOTRACE runs trace_bits too, with no moves: a separate branch here
       // made the compiler's task-loop structure hang on single-band pairs)
       BITS_PROG(0x40000000u);
+      if (a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
       trace_bits(a, pd, obuf_all[wid], lane, prog);
+      if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
       BITS_PROG(0x56000000u);
     }
   }
