@@ -1011,7 +1011,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   } fin;
   // Device finalize (nw_hash) when no input byte is '_' and the
   // batch has enough pairs for one lane per row to beat the host threads:
-  // est. device ms ~ 0.02 per 128-byte block of the longest row (per wave
+  // est. device ms ~ 0.007 per 128-byte block of the longest row (per wave
   // slot round), host ~ 350 bytes/us per thread.  NWK_DEVHASH=0/1 forces.
   static const int devhash_env = getenv("NWK_DEVHASH") ? atoi(getenv("NWK_DEVHASH")) : -1;
   const int fin_mode = c->opts.finalize == 1 ? 0 : c->opts.finalize == 2 ? 1 : devhash_env;
@@ -1079,9 +1079,11 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         maxlen = std::max(maxlen, (double)(dp[q].m + dp[q].n));
       }
       const double waves = 2.0 * np / 64.0, slots = 8.0 * c->cus;
-      const double est_dev = (maxlen / 128.0) * 0.02 * std::max(1.0, waves / slots);
+      // ~0.007 ms per 128-byte block of the longest row since nw_rows / nw_hash
+      // went to four waves per pair and bitop3 rounds (C3: 781 blocks, 5.5 ms)
+      const double est_dev = (maxlen / 128.0) * 0.007 * std::max(1.0, waves / slots);
       const double est_host = bytes / (350e3 * c->host_threads);
-      devhash = fin_mode == 1 || est_dev < 0.5 * est_host;
+      devhash = fin_mode == 1 || est_dev < 0.8 * est_host;
       st.device_finalized += devhash ? 1 : 0;
     }
     // Layout: [granules | slack | matrices | op strings].  The granule region
