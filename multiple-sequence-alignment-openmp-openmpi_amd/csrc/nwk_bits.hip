@@ -247,6 +247,10 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
     if (prog && lane == 0) __hip_atomic_store((gu32*)prog, (unsigned)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
   } while (0)
 
+// NWK_TRACE_PRIO 1: the traceback wave raises its issue priority (s_setprio 3)
+#ifndef NWK_TRACE_PRIO
+#define NWK_TRACE_PRIO 0
+#endif
 // NWK_TRACE_MASKS 1: a branch-free walk on per-row ballot masks (SGPR bit tests)
 // instead of two v_readlane per move.  Measured equal (C3 8-rank shard: 9.7-10.0
 // vs 9.5 ms per 100k-move trace: a lone wave issues about one instruction per
@@ -566,7 +570,14 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
       // made the compiler's task-loop structure hang on single-band pairs)
       BITS_PROG(0x40000000u);
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
+#if NWK_TRACE_PRIO
+      // the walk is one latency-bound wave: let it issue ahead of the SIMD's fill waves
+      __builtin_amdgcn_s_setprio(3);
+#endif
       trace_bits(a, pd, obuf_all[wid], lane, prog);
+#if NWK_TRACE_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
       BITS_PROG(0x56000000u);
     }
