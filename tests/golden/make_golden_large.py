@@ -8,6 +8,8 @@ independent and can run concurrently:
     python tests/golden/make_golden_large.py c3        # sub, ~75 min on 8 cores
     python tests/golden/make_golden_large.py c3_pairs  # skel_debug, first 9 seqs (36 pairs)
     python tests/golden/make_golden_large.py c4 c4_pairs
+    python tests/golden/make_golden_large.py c4_oracle # oracle, 8 processes, ~25 min (c4.json
+                                                       # as committed: sub would take ~9 h)
     python tests/golden/make_golden_large.py edge16    # skel_debug, 4 penalty pairs
     python tests/golden/make_golden_large.py c5_scores # oracle score-only, O(n) memory
 
@@ -69,6 +71,37 @@ def job_full(cfg):
                          "8-core build container): %d us" % us})
 
 
+def _oracle_pair(args):
+    x, y, pxy, pgap = args
+    p, a1, a2 = oracle.pair(x, y, pxy, pgap)
+    return p, oracle.problem_hash(a1, a2)
+
+
+def job_full_oracle(cfg, procs=8):
+    """The same answer from the C restatement (nw_oracle.c), pair-parallel over
+    `procs` processes: for C4, whose 32,640 pairs take sub's singleton rank
+    ~1 s each here (120 pairs of the config: 124 s), ~9 h.  The oracle is
+    pinned to the reference (golden.json, test_oracle.py), and on this config
+    its first 36 per-pair problemhashes must equal skel_debug's (c4_pairs.json)."""
+    from multiprocessing import Pool
+    desc, k, L, pxy, pgap, _ = workloads.SYNTH[cfg]
+    genes = workloads.synth(k, L)
+    args = [(genes[i], genes[j], pxy, pgap) for i in range(1, k) for j in range(i)]
+    t0 = time.time()
+    with Pool(procs) as pool:
+        res = pool.map(_oracle_pair, args, chunksize=32)
+    pens, hs = [r[0] for r in res], [r[1] for r in res]
+    ref = json.load(open(os.path.join(OUT, cfg + "_pairs.json")))
+    n = len(ref["pairs"])
+    assert [pp["problemhash"] for pp in ref["pairs"]] == hs[:n], "oracle disagrees with skel_debug"
+    assert ref["penalties"] == pens[:n], "oracle disagrees with skel_debug"
+    save(cfg, {"config": desc, "k": k, "L": L, "pxy": pxy, "pgap": pgap, "hash": oracle.chain(hs),
+               "penalties": pens,
+               "source": "oracle nw_oracle.c (skel:186-280 restatement), %d processes, %.0f s; first %d "
+                         "pairs' problemhashes = skel_debug's (%s_pairs.json). sub's singleton rank needs "
+                         "~1 s per 8k pair here (~9 h for the config)" % (procs, time.time() - t0, n, cfg)})
+
+
 def job_pairs(cfg, nseq=9):
     desc, k, L, pxy, pgap, _ = workloads.SYNTH[cfg]
     genes = workloads.synth(nseq, L)
@@ -112,6 +145,8 @@ def main(argv):
     for a in argv or ["c3", "c3_pairs", "c4", "c4_pairs", "edge16", "c5_scores"]:
         if a in ("c3", "c4"):
             job_full(a)
+        elif a in ("c3_oracle", "c4_oracle"):
+            job_full_oracle(a[:2])
         elif a in ("c3_pairs", "c4_pairs"):
             job_pairs(a[:2])
         elif a == "edge16":
