@@ -405,7 +405,8 @@ def main():
         "answer_source": expect["source"] if expect else None,
         "kernel": {"name": kernel, "fill_ms": round(fill_ms, 3), "traceback_ms": round(float(np.mean(traces)), 3),
                    "fill_gcups": round(my_cells / (fill_ms * 1e-3) / 1e9, 2),
-                   "fill_launches_per_step": st["fill_launches"], "batches": st["batches"]},
+                   "fill_launches_per_step": st["fill_launches"], "batches": st["batches"],
+                   "window_retries": st.get("window_retries", 0)},
         "roofline": roofline(args.workload if not args.affine else args.workload + "_affine", kernel,
                              fill_ms / launches * 1e-3, my_cells, launches),
     }
