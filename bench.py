@@ -197,13 +197,22 @@ def load_pmc(workload, kernel):
 
 
 def roofline(workload, kernel, launch_s, my_cells, launches):
+    import seqalign
+
     pmc = load_pmc(workload, kernel)
+    sid = seqalign.kernel_source_id(kernel)
     eq_gbs = my_cells * BYTES_PER_CELL / launches / launch_s / 1e9
     out = {"kernel": kernel, "launch_ms": round(launch_s * 1e3, 3),
-           "equivalent_4B_per_cell_GBps": round(eq_gbs, 1)}
+           "equivalent_4B_per_cell_GBps": round(eq_gbs, 1), "kernel_source_id": sid}
+    note = None
     if pmc is None:
+        note = "no profiles/r*/pmc_%s.json for %s" % (workload, kernel)
+    elif pmc.get("kernel_source_id") != sid:
+        note = ("%s holds counters of kernel build %s, this run's %s is %s: no counter roofline until the "
+                "PMC passes are re-run on this build" % (pmc["_file"], pmc.get("kernel_source_id"), kernel, sid))
+    if note:
         out.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
-                    "note": "no profiles/r*/pmc_%s.json for %s" % (workload, kernel)})
+                    "note": note})
         return out
     clk = pmc["grbm_gui_active_per_launch"] / 8.0 / (pmc["duration_ns_per_launch"] * 1e-9)  # Hz, 8 XCDs
     insts = pmc["sq_insts_valu_per_launch"]
@@ -245,10 +254,51 @@ def spawn_ranks(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    return wait_ranks(procs)
+
+
+def wait_ranks(procs, poll_s=0.05, grace_s=10.0):
+    """Waits for every rank process.  The first non-zero exit (in time, not in
+    rank order -- a peer blocked in init_process_group or the all-gather would
+    otherwise hold the launcher) terminates the others, then kills what is left
+    after grace_s; every child is reaped.  Returns that first failure code, or 0."""
     rc = 0
-    for p in procs:
-        rc = rc or p.wait()
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+                t_end = time.time() + grace_s
+                for q in live:
+                    try:
+                        q.wait(timeout=max(0.0, t_end - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                live = []
+                break
+        if live:
+            time.sleep(poll_s)
     return rc
+
+
+def mapped_libs():
+    keys = ("libamdhip64", "librccl", "libhsa-runtime64", "libnwk")
+    libs = set()
+    try:
+        for line in open("/proc/self/maps"):
+            path = line.split()[-1] if len(line.split()) >= 6 else ""
+            if any(k in os.path.basename(path) for k in keys):
+                libs.add(path)
+    except OSError:
+        pass
+    return sorted(libs)
 
 
 def main():
@@ -276,7 +326,11 @@ def main():
     dist = None
     coll_device = None
     gpu = local
-    if world > 1:
+    # NWK_BENCH_FORCE_DIST=1 (tests): the sharded path -- process group, LPT
+    # shard, the one all-gather -- even at WORLD_SIZE 1, so a 1-GPU box runs
+    # the RCCL collective the driver's N-GPU runs use
+    sharded = world > 1 or os.environ.get("NWK_BENCH_FORCE_DIST") == "1"
+    if sharded:
         import torch
         import torch.distributed as tdist
 
@@ -314,7 +368,7 @@ def main():
     ws = int(float(os.environ.get("NWK_BENCH_WS_GB", "0")) * (1 << 30))  # test hook: per-rank HBM budget
     eng = seqalign.Engine(device=gpu, bits=args.bits, verbose=args.verbose, workspace_bytes=ws)
     eng.set_sequences(genes)  # sequences resident in HBM before timing
-    my_ids = seqalign.shard_pairs(lengths, rank, world) if world > 1 else np.arange(P, dtype=np.int64)
+    my_ids = seqalign.shard_pairs(lengths, rank, world) if sharded else np.arange(P, dtype=np.int64)
 
     if affine:
         def align(ids, a, b):
@@ -323,7 +377,7 @@ def main():
         align = eng.align_pairs
 
     def step():
-        if world > 1:
+        if sharded:
             pen, hs, _ = nwdist.align_sharded(align, lengths, pxy, pgap, rank, world, device=coll_device)
             h = seqalign.chain_hash(hs) if rank == 0 else None
         else:  # getMinimumPenalties on the engine: the chain overlaps later batches
@@ -331,7 +385,7 @@ def main():
         return pen, h
 
     def sync():
-        if world > 1:
+        if sharded:
             import torch
 
             dist.barrier()
@@ -357,7 +411,7 @@ def main():
     sync()
     dt = time.perf_counter() - t0
     checks.append(check(pen, h))  # the last timed step's answer
-    if world > 1:
+    if sharded:
         import torch
 
         t = torch.tensor([dt], dtype=torch.float64, device=coll_device)
@@ -371,7 +425,7 @@ def main():
     ms_step = dt / max(args.steps, 1) * 1e3
     gcups = total_cells * args.steps / dt / 1e9
     st = eng.stats()
-    my_cells = workloads.cells(genes, my_ids) if world > 1 else total_cells
+    my_cells = workloads.cells(genes, my_ids) if sharded else total_cells
     fill_ms = float(np.mean(fills)) if fills else float("nan")
     launches = max(st["fill_launches"], 1)
     kernel = seqalign.KERNELS.get(st["mode"], "?")
@@ -410,6 +464,12 @@ def main():
         "roofline": roofline(args.workload if not args.affine else args.workload + "_affine", kernel,
                              fill_ms / launches * 1e-3, my_cells, launches),
     }
+    if sharded:
+        out["collective"] = {"backend": dist.get_backend(), "all_gathers_per_step": 1,
+                             "record_bytes": 72, "forced_at_world_1": world == 1}
+    # which HIP runtime / RCCL this process bound (torch, when imported first,
+    # brings its own libamdhip64 / librccl and libnwk.so binds to those)
+    out["runtime_libs"] = mapped_libs()
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(genes, pxy, pgap, affine)
     print(json.dumps(out), flush=True)

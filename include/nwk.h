@@ -63,7 +63,9 @@ typedef struct nwk_opts {
   int32_t kernel;            /* linear fill kernel: 0 auto (nw_align_bits where admissible: pxy >= 0, pgap 1 or 2,
                                 <= 4 symbols), 1 nw_align, 2 nw_align_pk, 3 nw_align_pk2, 4 nw_align_bits (a
                                 kernel where it is not exact -- W > 4, mixed-sign K, pgap > 2 -- falls back) */
-  int32_t reserved[2];
+  int32_t collective;        /* nwk_get_minimum_penalties: 1 = take the sharded RCCL all-gather path even when
+                                ngpus == 1 (one communicator of one rank; tests the collective on a 1-GPU box) */
+  int32_t reserved[1];
 } nwk_opts;
 
 typedef struct nwk_stats {
@@ -79,8 +81,8 @@ typedef struct nwk_stats {
   int32_t fill_launches;     /* fill-kernel launches in the call */
   int32_t device_finalized;  /* batches whose pairs were finalized on the device */
   int32_t linear_space_pairs; /* pairs aligned with the linear-space traceback */
-  int32_t window_retries;    /* nw_align_bits windowed storage: pairs re-run with full storage (path left the window) */
-  int32_t reserved[1];
+  int32_t window_retries;    /* windowed storage: pairs re-run wider (path left the window) */
+  int32_t window;            /* storage window W in columns of the call's first pairs (0 = full storage) */
 } nwk_stats;
 
 /* Defaults for nwk_opts (device 0, auto everything). */

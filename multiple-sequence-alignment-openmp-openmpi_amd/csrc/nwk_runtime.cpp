@@ -227,11 +227,13 @@ int nwk_ctx_create(const nwk_opts* opts, nwk_ctx** out) {
   nwk_opts_default(&o);
   if (opts) o = *opts;
   if (const char* v = getenv("NWK_VERBOSE")) o.verbose = atoi(v);  // debug: diagnostics on stderr
-  if (ndev <= 0) return fail(NWK_EDEVICE, "nwk_ctx_create: no HIP device visible");
-  if (o.device < 0 || o.device >= ndev) return fail(NWK_EINVAL, "nwk_ctx_create: device %d of %d", o.device, ndev);
+  // option checks first: they need no device
   if (o.finalize < 0 || o.finalize > 2) return fail(NWK_EINVAL, "nwk_ctx_create: finalize must be 0/1/2");
+  if (o.kernel < 0 || o.kernel > 4) return fail(NWK_EINVAL, "nwk_ctx_create: kernel must be 0..4");
   if (o.bits != 0 && o.bits != 4 && o.bits != 8 && o.bits != 16 && o.bits != 32)
     return fail(NWK_EINVAL, "nwk_ctx_create: bits must be 0/4/8/16/32");
+  if (ndev <= 0) return fail(NWK_EDEVICE, "nwk_ctx_create: no HIP device visible");
+  if (o.device < 0 || o.device >= ndev) return fail(NWK_EINVAL, "nwk_ctx_create: device %d of %d", o.device, ndev);
   std::unique_ptr<nwk_ctx> c(new nwk_ctx);
   c->opts = o;
   c->device = o.device;
@@ -463,10 +465,11 @@ int choose_plan(const nwk_ctx* c, const Scoring& sc, Plan* pl) {
   if (pl->mode == kProfile && pl->bits == 4 && packed > 0 && ((pl->K0 < 0) == (pl->K1 < 0)))
     pl->mode = packed == 1 ? kPacked : kPacked2;
   // bit-sliced difference planes (nw_align_bits) wherever they apply: pxy >= 0,
-  // pgap in {1, 2}, <= 4 symbols.  opts.kernel 4 (or NWK_BITS=1) asks for it,
-  // 1..3 pin the integer kernels, NWK_BITS=0 disables it under "auto".
+  // pgap in {1, 2}, <= 4 symbols.  opts.kernel 4 asks for it, 1..3 pin the
+  // integer kernels, NWK_BITS_KERNEL=0 disables it under "auto" (A/B runs; the
+  // driver's NWK_BITS is the storage width, opts.bits).
   // pl->bits keeps the profile kernels' width (the linear-space path uses it).
-  static const int bits_env = getenv("NWK_BITS") ? atoi(getenv("NWK_BITS")) : 1;
+  static const int bits_env = getenv("NWK_BITS_KERNEL") ? atoi(getenv("NWK_BITS_KERNEL")) : 1;
   const bool want_bits = c->opts.kernel == 4 || (c->opts.kernel == 0 && bits_env != 0);
   if (want_bits && c->opts.bits == 0 && bits_admissible(pxy, pgap, c->alpha)) pl->mode = kBits;
   return NWK_OK;
@@ -519,6 +522,23 @@ int64_t pka_nsb_of(int m, int n, int w) {
   const int64_t all = sblocks_of(kAffinePk, ceil_div(n, 64));
   if (w <= 0) return all;
   return std::min(all, ceil_div(ceil_div((int64_t)2 * kBandRows * n, m) + 2 * (int64_t)w + 256, 64) + 2);
+}
+
+// Storage window W of a job whose full matrices exceed the budget (see
+// align_work).  kBits: the widest candidate whose whole job fits `batches`
+// batches (1 unless NWK_WIN_BATCHES), at least 1024.  kAffinePk: 8192
+// outright -- its paths stray up to ~4.6k columns (profiles/r02/pathdev_c5.txt)
+// and it needs many rounds of band-pair tasks per batch anyway.  need(W) is
+// the job's bytes at window W.  (Compares need / batches against the budget:
+// batches x budget overflowed int64 for large budgets.)
+template <class Need>
+int choose_window(int mode, int batches, int64_t budget, Need&& need) {
+  if (mode == kAffinePk && batches <= 0) return 8192;
+  const int64_t nb = batches > 0 ? batches : 1;
+  static const int cand[] = {8192, 6144, 4096, 3072, 2560, 2048, 1536, 1024};
+  for (int wc : cand)
+    if (ceil_div(need(wc), nb) <= budget) return wc;
+  return 1024;
 }
 
 void footprint(PairWork* w, int bits, int mode, bool affine) {
@@ -886,7 +906,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   // whose path leaves its window is appended once, and the async finalize
   // holds pointers into dp, so it must never reallocate)
   std::vector<PairWork> dp;
-  dp.reserve(2 * work.size());
+  dp.reserve(4 * work.size() + 16);
   for (auto& w : work) {
     st.cells += (double)w.m * (double)w.n;
     if (w.m == 0 || w.n == 0) {
@@ -927,7 +947,6 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   static const int win_env = getenv("NWK_BITS_WIN") ? atoi(getenv("NWK_BITS_WIN")) : -1;
   static const int winb_env = getenv("NWK_WIN_BATCHES") ? atoi(getenv("NWK_WIN_BATCHES")) : 0;
   if ((pl.mode == kBits || pl.mode == kAffinePk) && !dp.empty() && win_env != 0) {
-    const int64_t nbat = winb_env > 0 ? winb_env : pl.mode == kAffinePk ? (int64_t)1 << 30 : 1;
     auto total_b = [&]() {
       int64_t mat = 0, bnd = 0, ops = 0;
       for (const auto& w : dp) mat += w.mat_dw, bnd += w.bnd_gr, ops += w.ops_b;
@@ -940,19 +959,14 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       }
     };
     int W = win_env > 0 ? win_env : 0;
-    if (W == 0 && total_b() > c->budget) {
-      static const int cand[] = {8192, 6144, 4096, 3072, 2560, 2048, 1536, 1024};
-      for (int wc : cand) {
+    if (W == 0 && total_b() > c->budget)
+      W = choose_window(pl.mode, winb_env, c->budget, [&](int wc) {
         set_w(wc);
-        if (total_b() <= nbat * c->budget) {
-          W = wc;
-          break;
-        }
-      }
-      if (W == 0) W = 1024;
-    }
+        return total_b();
+      });
     set_w(W);
   }
+  st.window = dp.empty() ? 0 : dp[0].bits_w;
   // Largest first (LPT inside the device; longest bands dequeued first).
   // kPacked2 (NWK_SORT != 0): by traceback length m + n first, so the pairs
   // filled last -- whose traces form the kernel's tail -- are the shortest to trace.
@@ -1430,9 +1444,34 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         if (skip.empty()) skip.assign((size_t)np, 0);
         skip[q] = 1;
         PairWork w = dp[pos + q];
+        const int old_w = w.bits_w;
         w.bits_w = 0;
         footprint(&w, pl.bits, pl.mode, sc.affine);
-        dp.push_back(w);  // capacity reserved: no reallocation
+        auto need = [](const PairWork& x) {
+          return x.mat_dw * 4 + x.bnd_gr * 8 + 3 * x.ops_b + x.segops_b + 8192;
+        };
+        if (pl.mode == kAffinePk && need(w) > c->budget) {
+          // the affine path has no linear-space fallback: re-run with the
+          // widest doubled window that fits the budget instead of in full
+          int nw = 0;
+          for (int64_t cw = 2 * (int64_t)old_w; cw < (1 << 30); cw *= 2) {
+            PairWork t = w;
+            t.bits_w = (int)cw;
+            footprint(&t, pl.bits, pl.mode, sc.affine);
+            if (need(t) > c->budget) break;
+            nw = (int)cw;
+            if (t.mat_dw >= w.mat_dw) break;  // as wide as full storage
+          }
+          if (nw == 0)
+            return fail(NWK_ENOMEM, "pair %lld (%d x %d): its traceback left the %d-column storage window and "
+                        "neither full storage (%lld B) nor a %d-column window fits the HBM budget %lld",
+                        (long long)w.id, w.m, w.n, old_w, (long long)need(w), 2 * old_w, (long long)c->budget);
+          w.bits_w = nw;
+          footprint(&w, pl.bits, pl.mode, sc.affine);
+        }
+        if (dp.size() == dp.capacity())  // the async finalize holds pointers into dp
+          return fail(NWK_ENOMEM, "pair %lld: too many window re-runs", (long long)w.id);
+        dp.push_back(w);
         st.window_retries += 1;
       }
     }
@@ -1710,7 +1749,7 @@ static int min_penalties_sc(const uint8_t* seqs, const int64_t* offsets, int32_t
     hash_hex[0] = 0;
     return NWK_OK;
   }
-  if (G == 1) {
+  if (G == 1 && !o.collective) {
     nwk_ctx* c = nullptr;
     int rc = nwk_ctx_create(&o, &c);
     if (rc != NWK_OK) return rc;

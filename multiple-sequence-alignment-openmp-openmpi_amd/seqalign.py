@@ -40,7 +40,8 @@ class Opts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("ngpus", ctypes.c_int32), ("bits", ctypes.c_int32),
                 ("host_threads", ctypes.c_int32), ("workspace_bytes", ctypes.c_int64),
                 ("verbose", ctypes.c_int32), ("finalize", ctypes.c_int32),
-                ("linear_space", ctypes.c_int32), ("kernel", ctypes.c_int32), ("reserved", ctypes.c_int32 * 2)]
+                ("linear_space", ctypes.c_int32), ("kernel", ctypes.c_int32), ("collective", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 1)]
 
 
 class Stats(ctypes.Structure):
@@ -50,7 +51,7 @@ class Stats(ctypes.Structure):
                 ("bits", ctypes.c_int32), ("mode", ctypes.c_int32),
                 ("fill_launches", ctypes.c_int32), ("device_finalized", ctypes.c_int32),
                 ("linear_space_pairs", ctypes.c_int32), ("window_retries", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("window", ctypes.c_int32)]
 
 
 # Every exported symbol of include/nwk.h with its ctypes signature.
@@ -80,6 +81,30 @@ SIGNATURES = {
 }
 
 _lib = None
+
+# Source files that determine each fill kernel's code object (plus the build
+# flags in the Makefile): kernel_source_id() hashes them, so a roofline's
+# per-launch counters (profiles/<round>/pmc_<workload>.json) can be tied to the
+# kernel build that produced them.
+KERNEL_SOURCES = {
+    "nw_align_bits": ("csrc/nwk_bits.hip", "csrc/nwk_internal.h", "Makefile"),
+    "nw_align_pka": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
+    "nw_align_pk2": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
+    "nw_align_pk": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
+    "nw_align_affine": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
+    "nw_align": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
+}
+
+
+def kernel_source_id(kernel):
+    """sha256 (16 hex digits) of the sources a fill kernel is compiled from."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES.get(kernel, ()):
+        with open(os.path.join(HERE, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16] if kernel in KERNEL_SOURCES else None
 
 
 def load_library(path=LIB_PATH):
@@ -331,8 +356,10 @@ def shard_pairs(lengths, rank, world):
     return out[:n.value].copy()
 
 
-def getMinimumPenalties(genes, k, pxy, pgap, penalties, ngpus=1, bits=0, verbose=False):
-    """skel:117-175: fills penalties[0..P) in canonical order, returns the hash."""
+def getMinimumPenalties(genes, k, pxy, pgap, penalties, ngpus=1, bits=0, verbose=False, collective=False):
+    """skel:117-175: fills penalties[0..P) in canonical order, returns the hash.
+    ngpus > 1 (or collective=True) shards the pairs over devices 0..ngpus-1 and
+    collects the result records with one in-process ncclAllGather."""
     lib = load_library()
     genes = list(genes)[:k]
     data, offs = pack_genes(genes)
@@ -341,7 +368,7 @@ def getMinimumPenalties(genes, k, pxy, pgap, penalties, ngpus=1, bits=0, verbose
     out = ctypes.create_string_buffer(129)
     o = Opts()
     lib.nwk_opts_default(ctypes.byref(o))
-    o.ngpus, o.bits, o.verbose = ngpus, bits, int(verbose)
+    o.ngpus, o.bits, o.verbose, o.collective = ngpus, bits, int(verbose), int(collective)
     _check(lib.nwk_get_minimum_penalties(_ptr(data), _ptr(offs), k, pxy, pgap, _ptr(pen), out,
                                          ctypes.byref(o)))
     for p in range(P):

@@ -102,6 +102,59 @@ def job_full_oracle(cfg, procs=8):
                          "~1 s per 8k pair here (~9 h for the config)" % (procs, time.time() - t0, n, cfg)})
 
 
+def _skel_pair(args):
+    """Pair p = (i, j) of a config through the reference program itself:
+    skel_debug on the two-sequence input [genes[j], genes[i]], whose only pair
+    (1, 0) has x = genes[i] (rows), y = genes[j] (columns) -- the same DP as
+    canonical pair p of the full input (skel:122-130)."""
+    p, xi, yj, pxy, pgap = args
+    _, pens, pairs = run_skel(workloads.token_text(pxy, pgap, [yj, xi]).decode("latin-1"), debug=True,
+                              timeout=3600)
+    assert len(pairs) == 1 and pens == [pairs[0]["penalty"]]
+    return p, pairs[0]["penalty"], pairs[0]["problemhash"]
+
+
+def job_full_skel(cfg, procs=6):
+    """The full answer from the reference program itself, pair-parallel: every
+    canonical pair through skel_debug as a two-sequence job (_skel_pair), then
+    the chain of skel:159 over the per-pair problemhashes.  C4 (32,640 pairs of
+    8k x 8k, ~0.4 s each for the serial skel) takes ~40 min on 6 processes --
+    against ~9 h for sub's singleton rank.  Progress is checkpointed to
+    /tmp/<cfg>_skel.jsonl so an interrupted run resumes."""
+    from multiprocessing import Pool
+    desc, k, L, pxy, pgap, _ = workloads.SYNTH[cfg]
+    genes = workloads.synth(k, L)
+    P = k * (k - 1) // 2
+    ck = "/tmp/%s_skel.jsonl" % cfg
+    done = {}
+    if os.path.exists(ck):
+        for line in open(ck):
+            r = json.loads(line)
+            done[r[0]] = (r[1], r[2])
+    todo = []
+    p = 0
+    for i in range(1, k):
+        for j in range(i):
+            if p not in done:
+                todo.append((p, genes[i], genes[j], pxy, pgap))
+            p += 1
+    t0 = time.time()
+    with Pool(procs) as pool, open(ck, "a") as f:
+        for n, (p, pen, ph) in enumerate(pool.imap_unordered(_skel_pair, todo, chunksize=4)):
+            done[p] = (pen, ph)
+            f.write(json.dumps([p, pen, ph]) + "\n")
+            if n % 500 == 0:
+                f.flush()
+                print("%s skel: %d/%d pairs, %.0f s" % (cfg, len(done), P, time.time() - t0), file=sys.stderr)
+    pens = [done[p][0] for p in range(P)]
+    hs = [done[p][1] for p in range(P)]
+    h = oracle.chain(hs)
+    save(cfg, {"config": desc, "k": k, "L": L, "pxy": pxy, "pgap": pgap, "hash": h, "penalties": pens,
+               "source": "oracle/_ref/skel_debug (root seqalign-mpi-skeleton.cpp, the reference's own "
+                         "program): every pair as a two-sequence job, %d processes, %.0f s; answer = the "
+                         "skel:159 chain over its per-pair problemhashes" % (procs, time.time() - t0)})
+
+
 def job_pairs(cfg, nseq=9):
     desc, k, L, pxy, pgap, _ = workloads.SYNTH[cfg]
     genes = workloads.synth(nseq, L)
@@ -147,6 +200,8 @@ def main(argv):
             job_full(a)
         elif a in ("c3_oracle", "c4_oracle"):
             job_full_oracle(a[:2])
+        elif a == "c4_skel":
+            job_full_skel("c4")
         elif a in ("c3_pairs", "c4_pairs"):
             job_pairs(a[:2])
         elif a == "edge16":

@@ -48,6 +48,24 @@ def test_world_size_must_match_gpus():
     assert r.returncode != 0 and b"WORLD_SIZE=2" in r.stderr
 
 
+def test_rank_launcher_stops_peers_on_first_failure():
+    """bench.wait_ranks: the first rank to fail (rank 2 here, while ranks 0 and
+    1 would block for a minute, as in a collective whose peer died) ends the
+    launch with its exit code; the peers are terminated and reaped."""
+    import time
+
+    import bench
+
+    procs = [subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"]) for _ in range(2)]
+    procs.append(subprocess.Popen([sys.executable, "-c", "import sys, time; time.sleep(0.5); sys.exit(3)"]))
+    t0 = time.time()
+    assert bench.wait_ranks(procs, grace_s=5.0) == 3
+    assert time.time() - t0 < 30
+    assert all(p.returncode is not None for p in procs)
+    ok = [subprocess.Popen([sys.executable, "-c", "pass"]) for _ in range(3)]
+    assert bench.wait_ranks(ok) == 0
+
+
 @pytest.mark.gpu
 def test_two_ranks_share_one_gpu_big13_published_hash():
     env = _env(NWK_BENCH_BACKEND="gloo", NWK_BENCH_SHARE_GPU="1", NWK_BENCH_WS_GB="110")
@@ -59,3 +77,35 @@ def test_two_ranks_share_one_gpu_big13_published_hash():
     assert line["n_gpus"] == 2
     assert line["answer_hash_ok"] is True
     assert line["kernel"]["name"].startswith("nw_align")
+
+
+@pytest.mark.gpu
+def test_bench_nccl_all_gather_at_world_one():
+    """The driver's multi-GPU bench path with the real backend: torch.distributed
+    over "nccl" (= RCCL), LPT shard, ONE all_gather_into_tensor of the 72-byte
+    records and the max-over-ranks all_reduce, forced at WORLD_SIZE 1
+    (NWK_BENCH_FORCE_DIST) so it runs on a 1-GPU box; big13's published hash.
+    The JSON line names the HIP runtime and RCCL the process mapped (torch is
+    imported first, so libnwk.so binds to torch's)."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = _env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               NWK_BENCH_FORCE_DIST="1", NWK_BENCH_WS_GB="110")
+    r = subprocess.run([sys.executable, "-u", BENCH, "--gpus", "1", "--workload", "big13", "--steps", "2",
+                        "--warmup", "1", "--no-cpu-baseline"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       env=env, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.decode().strip().split("\n")[-1])
+    assert line["answer_hash_ok"] is True
+    assert line["collective"]["backend"] == "nccl"
+    libs = line["runtime_libs"]
+    print("runtime libraries mapped:", libs)
+    assert any("librccl" in x for x in libs) and any("libamdhip64" in x for x in libs)
+    out = os.path.join(REPO, "gpurun_out")
+    if os.path.isdir(out):
+        with open(os.path.join(out, "bench_nccl_world1.json"), "w") as f:
+            f.write(json.dumps(line) + "\n")

@@ -245,6 +245,47 @@ def test_affine_packed_windowed_storage_and_full_rerun(win):
             assert o["retries"] > 0, "a 40-column window must send some pairs to the full re-run"
 
 
+_AFF_WIDEN_SCRIPT = r"""
+import json, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import seqalign, workloads
+genes = workloads.synth(2, 20000)
+out = []
+for ws in (150 << 20, 4 << 30):
+    with seqalign.Engine(device=0, workspace_bytes=ws) as e:
+        e.set_sequences(genes)
+        pen, hs = e.align_pairs_affine(np.arange(1, dtype=np.int64), 3, 3, 1)
+        st = e.stats()
+    out.append({"mode": st["mode"], "batches": st["batches"], "retries": st["window_retries"],
+                "pen": [int(v) for v in pen], "hs": [x.tobytes().hex() for x in hs]})
+print(json.dumps(out))
+"""
+
+
+def test_affine_window_rerun_widens_when_full_storage_does_not_fit():
+    """A windowed nw_align_pka pair whose trace leaves its window re-runs
+    with full storage -- or, when full storage does not fit the budget (affine
+    has no linear-space path), with the widest doubled window that does.  A
+    20k x 20k pair forced to a 32-column window (NWK_BITS_WIN) under a 150 MiB
+    budget (full storage ~206 MB, a 4096-column window ~101 MB) must still align, identically to the same pair
+    re-run in full under 4 GiB, with the oracle's O(n)-memory affine score."""
+    import json
+    import sys
+
+    import workloads
+
+    env = dict(os.environ, NWK_BITS_WIN="32")
+    res = subprocess.run([sys.executable, "-c", _AFF_WIDEN_SCRIPT, os.path.dirname(seqalign.__file__)],
+                         env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
+    assert res.returncode == 0, res.stderr.decode()[-2000:]
+    small, big = json.loads(res.stdout.decode().strip().splitlines()[-1])
+    assert small["mode"] == 7 and small["retries"] >= 1 and big["retries"] >= 1
+    assert small["pen"] == big["pen"] and small["hs"] == big["hs"]
+    genes = workloads.synth(2, 20000)
+    assert small["pen"] == [oracle.score_affine(genes[1], genes[0], 3, 3, 1)]
+
+
 def test_subset_and_order_of_pair_ids(engine):
     r = random.Random(5)
     genes = _rand_genes(r, 7, 50, 900, ACGT)
@@ -310,6 +351,19 @@ def test_multi_gpu_allgather_inprocess(golden):
     pxy, pgap, genes = case_input(c)
     pens = [0] * len(c["penalties"])
     h = seqalign.getMinimumPenalties(genes, len(genes), pxy, pgap, pens, ngpus=2)
+    assert h == c["hash"] and pens == c["penalties"]
+
+
+@pytest.mark.parametrize("name", ["xulin_test", "big13"])
+def test_inprocess_rccl_allgather_one_gpu(golden, name):
+    """The in-process multi-GPU path of nwk_get_minimum_penalties (one host
+    thread per device, ncclCommInitAll + ONE ncclAllGather of 72-byte records,
+    rank-0 chain; replaces sub:296-350) forced at one device (opts.collective),
+    so the RCCL code runs on a 1-GPU box: the reference's published answers."""
+    c = golden[name]
+    pxy, pgap, genes = case_input(c)
+    pens = [0] * len(c["penalties"])
+    h = seqalign.getMinimumPenalties(genes, len(genes), pxy, pgap, pens, ngpus=1, collective=True)
     assert h == c["hash"] and pens == c["penalties"]
 
 

@@ -111,6 +111,25 @@ def test_c5_affine_scores_vs_oracle(engine):
     assert [int(v) for v in pl] == [s["linear_penalty"] for s in g["scores"]]
 
 
+def test_affine_window_choice_at_a_large_budget():
+    """nw_align_pka's storage window at a budget above 2^33 B (the runtime used
+    to multiply the budget by 2^30 and overflow there): k=8 x 30k affine needs
+    ~13 GB at full storage, so a 9 GiB budget must pick W = 8192 (one batch, no
+    re-runs); pairs 0 and 1 against the oracle's O(n)-memory affine score."""
+    import oracle
+
+    genes = workloads.synth(8, 30000)
+    with seqalign.Engine(device=0, workspace_bytes=9 << 30) as e:
+        e.set_sequences(genes)
+        pa, _ = e.align_pairs_affine(np.arange(28, dtype=np.int64), 3, 3, 1)
+        st = e.stats()
+    assert st["mode"] == 7 and st["window"] == 8192, st
+    assert st["batches"] == 1 and st["window_retries"] == 0, st
+    for p in (0, 1):
+        i, j = seqalign.pair_ij(p)
+        assert int(pa[p]) == oracle.score_affine(genes[i], genes[j], 3, 3, 1)
+
+
 def _edge_cases():
     f = os.path.join(LARGE, "edge16.json")
     return json.load(open(f))["cases"] if os.path.exists(f) else []

@@ -126,6 +126,21 @@ def test_no_device_fails_loudly(lib):
         seqalign.getMinimumPenalties([b"AC", b"CA"], 2, 3, 2, [0])
 
 
+@pytest.mark.parametrize("field,value", [("kernel", 5), ("kernel", -1), ("finalize", 3), ("bits", 5)])
+def test_ctx_create_rejects_bad_options(lib, field, value):
+    """nwk_ctx_create checks its options before looking for a device: a bad
+    kernel / finalize / bits value is NWK_EINVAL with or without a GPU."""
+    import ctypes
+
+    o = seqalign.Opts()
+    lib.nwk_opts_default(ctypes.byref(o))
+    setattr(o, field, value)
+    ctx = ctypes.c_void_p()
+    assert lib.nwk_ctx_create(ctypes.byref(o), ctypes.byref(ctx)) == -1
+    assert field in lib.nwk_last_error().decode()
+    assert not ctx.value
+
+
 def test_parse_fasta_records():
     """FASTA input -- records in order, wrapped lines joined, blanks/comments skipped."""
     text = b">s1 first\nACGT\nAC GT\n\n>s2\n;comment\nTTTT\n>empty\n>s4\r\nGG\r\n"

@@ -24,6 +24,8 @@ import sys
 src, wl, kernel, rnd = sys.argv[1:5]
 suffix = sys.argv[5] if len(sys.argv) > 5 else ""
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "multiple-sequence-alignment-openmp-openmpi_amd"))
+import seqalign  # noqa: E402  (kernel_source_id: no library load)
 
 
 def per_dispatch(pattern):
@@ -51,6 +53,9 @@ write, _ = per_dispatch("pmc_write_" + wl + suffix)
 out = {
     "workload": wl + suffix,
     "kernel": kernel,
+    # the kernel build these counters belong to (bench.py reports frac null on a mismatch);
+    # run this script on the tree the passes ran on
+    "kernel_source_id": seqalign.kernel_source_id(kernel),
     "launches_measured": [len(valu), len(fetch), len(write)],
     "sq_insts_valu_per_launch": mean(v["SQ_INSTS_VALU"] for v in valu.values()),
     "sq_active_inst_valu_per_launch": mean(v["SQ_ACTIVE_INST_VALU"] for v in valu.values()),
