@@ -135,10 +135,13 @@ __device__ __forceinline__ void bits_diffs(const unsigned (&X)[NP], const unsign
 //   H, V     h and v planes of the previous step
 //   cons     LDS: band-above row, entry (column & 63) * NP + k (bit 31)
 //   ring     LDS: this band's last row, entry (column & 127) * NP + k (bit 31)
+//   eh       MASK blocks: this lane's bit-0 column at step s0 (columns < 0 keep
+//            v = 0; strips: the column within the current row pass, so a bit
+//            entering column 0 of its next pass sees the left border)
 template <int NP, int SR, bool MASK, bool PROD>
 __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsigned x1, unsigned yp0, unsigned yp1,
                                            unsigned w0, unsigned w1, unsigned (&H)[NP], unsigned (&V)[NP],
-                                           const unsigned* cons, unsigned* ring, unsigned* st, bool sto) {
+                                           const unsigned* cons, unsigned* ring, unsigned* st, bool sto, int eh) {
   unsigned dw[8], uw[8];
   // the band-above entries are read one step ahead (an LDS read's latency
   // would otherwise sit on every step's dependence chain)
@@ -214,7 +217,7 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
     uw[q] = V[0];
 #endif
     if constexpr (MASK) {  // columns < 0 keep v = 0 (the left border seen by column 0)
-      const int e = s - 32 * lane;
+      const int e = eh + q;
       const unsigned M = e >= 31 ? ~0u : (e < 0 ? 0u : (2u << e) - 1u);
 #pragma unroll
       for (int k = 0; k < NP; ++k) V[k] &= M;
@@ -519,12 +522,13 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
         const int rel = (s0 >> 3) - blo;
         const bool sto = (unsigned)rel < (unsigned)nblk;
         unsigned* st = mb + (int64_t)rel * 1024;
+        const int eh = s0 - 32 * lane;
         if (mask) {
-          if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto);
-          else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto);
+          if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh);
+          else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh);
         } else {
-          if (prod) bits_block<NP, SR, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto);
-          else bits_block<NP, SR, false, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto);
+          if (prod) bits_block<NP, SR, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh);
+          else bits_block<NP, SR, false, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh);
         }
         if ((blk & 3) == 3) {  // end of a 32-step half: its window becomes the previous one
           yp0 = w0;
