@@ -301,6 +301,12 @@ def mapped_libs():
     return sorted(libs)
 
 
+def nwdist_auto_chunks(P, world):
+    import dist as nwdist
+
+    return nwdist.auto_chunks(P, world)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -376,12 +382,24 @@ def main():
     else:
         align = eng.align_pairs
 
+    # sharded linear runs: the shard in `chunks` pieces, each piece's records
+    # all-gathered (and chained on rank 0) while the next piece aligns
+    chunks = int(os.environ.get("NWK_BENCH_CHUNKS", "0")) or nwdist_auto_chunks(P, world)
+    piece_stats = []
+
     def step():
-        if sharded:
+        del piece_stats[:]
+        if sharded and not affine:
+            h, pen, _ = nwdist.align_sharded_pipelined(eng, lengths, pxy, pgap, rank, world, chunks=chunks,
+                                                       device=coll_device,
+                                                       on_piece=lambda c: piece_stats.append(eng.stats()))
+        elif sharded:
             pen, hs, _ = nwdist.align_sharded(align, lengths, pxy, pgap, rank, world, device=coll_device)
             h = seqalign.chain_hash(hs) if rank == 0 else None
+            piece_stats.append(eng.stats())
         else:  # getMinimumPenalties on the engine: the chain overlaps later batches
             h, pen, _ = eng.align_all(pxy, pgap, affine=(go, ge) if affine else None)
+            piece_stats.append(eng.stats())
         return pen, h
 
     def sync():
@@ -403,11 +421,12 @@ def main():
     sync()
     fills, traces = [], []
     t0 = time.perf_counter()
+    launches = 0
     for _ in range(args.steps):
         pen, h = step()
-        st = eng.stats()
-        fills.append(st["fill_ms"])
-        traces.append(st["traceback_ms"])
+        fills.append(sum(x["fill_ms"] for x in piece_stats))
+        traces.append(sum(x["traceback_ms"] for x in piece_stats))
+        launches = sum(x["fill_launches"] for x in piece_stats)
     sync()
     dt = time.perf_counter() - t0
     checks.append(check(pen, h))  # the last timed step's answer
@@ -427,7 +446,7 @@ def main():
     st = eng.stats()
     my_cells = workloads.cells(genes, my_ids) if sharded else total_cells
     fill_ms = float(np.mean(fills)) if fills else float("nan")
-    launches = max(st["fill_launches"], 1)
+    launches = max(launches, 1)
     kernel = seqalign.KERNELS.get(st["mode"], "?")
     answer_ok = None if expect is None else all(c is True for c in checks)
     out = {
@@ -447,26 +466,28 @@ def main():
                  if st["mode"] == 7 else
                  "u32 bit planes (bit-sliced: 32 cells per VALU op, 2*pgap thermometer planes of the "
                  "G-space differences; int32-exact results, 2-bit traceback storage)"
-                 if st["mode"] == 8 else ("int32" if st["bits"] == 32 else
+                 if st["mode"] in (8, 9) else ("int32" if st["bits"] == 32 else
                                               "int32 (%d-bit mod-2^W traceback storage)" % st["bits"]),
         "data": "reference input file (mseq-big13-example.txt)" if args.workload == "big13"
                 else "synthetic (seeded MT19937 ACGT, workloads.py)",
         "config": {"workload": name, "pairs": P, "cells": total_cells, "pxy": pxy,
                    "gaps": ("affine go=%d ge=%d" % (go, ge)) if affine else "linear pgap=%d" % pgap,
                    "storage_bits_per_cell": st["bits"], "mode": seqalign.MODES.get(st["mode"]),
-                   "parallelism": "pair-sharded dp%d (LPT), one all-gather" % world},
+                   "parallelism": "pair-sharded dp%d (LPT), %d all-gather(s) of 72-B records, chain streamed on rank 0" % (world, chunks if sharded and not affine else 1)},
         "answer_hash_ok": answer_ok,
         "answer_source": expect["source"] if expect else None,
         "kernel": {"name": kernel, "fill_ms": round(fill_ms, 3), "traceback_ms": round(float(np.mean(traces)), 3),
                    "fill_gcups": round(my_cells / (fill_ms * 1e-3) / 1e9, 2),
-                   "fill_launches_per_step": st["fill_launches"], "batches": st["batches"],
-                   "window_retries": st.get("window_retries", 0)},
+                   "fill_launches_per_step": launches, "batches": sum(x["batches"] for x in piece_stats),
+                   "window_retries": sum(x.get("window_retries", 0) for x in piece_stats),
+                   "window": st.get("window", 0)},
         "roofline": roofline(args.workload if not args.affine else args.workload + "_affine", kernel,
                              fill_ms / launches * 1e-3, my_cells, launches),
     }
     if sharded:
-        out["collective"] = {"backend": dist.get_backend(), "all_gathers_per_step": 1,
-                             "record_bytes": 72, "forced_at_world_1": world == 1}
+        out["collective"] = {"backend": dist.get_backend(), "all_gathers_per_step": 1 if affine else chunks,
+                             "record_bytes": 72, "forced_at_world_1": world == 1,
+                             "pieces_per_rank": 1 if affine else chunks}
     # which HIP runtime / RCCL this process bound (torch, when imported first,
     # brings its own libamdhip64 / librccl and libnwk.so binds to those)
     out["runtime_libs"] = mapped_libs()

@@ -61,8 +61,11 @@ typedef struct nwk_opts {
   int32_t linear_space;      /* linear-space traceback: 0 = only for pairs whose matrix exceeds
                                 the HBM budget, -1 = never, G > 0 = every pair, G bands per recompute group */
   int32_t kernel;            /* linear fill kernel: 0 auto (nw_align_bits where admissible: pxy >= 0, pgap 1 or 2,
-                                <= 4 symbols), 1 nw_align, 2 nw_align_pk, 3 nw_align_pk2, 4 nw_align_bits (a
-                                kernel where it is not exact -- W > 4, mixed-sign K, pgap > 2 -- falls back) */
+                                <= 4 symbols -- as 2048-row band tasks or, for jobs of many pairs per wave slot, as
+                                one rolling strip per pair, nw_align_strip), 1 nw_align, 2 nw_align_pk,
+                                3 nw_align_pk2, 4 nw_align_bits band tasks, 5 nw_align_strip wherever admissible
+                                (n / 64 in [63, 200] for pgap 2, [63, 500] for pgap 1; a kernel where it is not
+                                exact -- W > 4, mixed-sign K, pgap > 2 -- falls back) */
   int32_t collective;        /* nwk_get_minimum_penalties: 1 = take the sharded RCCL all-gather path even when
                                 ngpus == 1 (one communicator of one rank; tests the collective on a 1-GPU box) */
   int32_t reserved[1];
@@ -77,7 +80,7 @@ typedef struct nwk_stats {
   int32_t batches;           /* workspace batches used */
   int32_t bits;              /* storage width used */
   int32_t mode;              /* 0 = profile, 1 = compare, 2 = literal, 3 = affine, 4 = packed profile, 5 = packed band
-                                pairs, 7 = packed affine band pairs, 8 = bit-sliced planes */
+                                pairs, 7 = packed affine band pairs, 8 = bit-sliced planes, 9 = bit-sliced strips */
   int32_t fill_launches;     /* fill-kernel launches in the call */
   int32_t device_finalized;  /* batches whose pairs were finalized on the device */
   int32_t linear_space_pairs; /* pairs aligned with the linear-space traceback */
@@ -112,6 +115,16 @@ int nwk_set_sequences(nwk_ctx *ctx, const uint8_t *seqs, const int64_t *offsets,
  */
 int nwk_align_pairs(nwk_ctx *ctx, const int64_t *pair_ids, int64_t npairs, int32_t pxy,
                     int32_t pgap, int32_t *penalties, uint8_t *problem_hash);
+
+/*
+ * nwk_align_pairs in two halves: _begin launches the call on a host thread of
+ * the context and returns at once; _end waits for it and writes penalties[n]
+ * and problem_hash[n*64] (order of pair_ids).  Between the two the context
+ * must not be used (one call in flight).  A rank overlaps its exchange and the
+ * chain of one chunk of its shard with the alignment of the next this way.
+ */
+int nwk_align_pairs_begin(nwk_ctx *ctx, const int64_t *pair_ids, int64_t npairs, int32_t pxy, int32_t pgap);
+int nwk_align_pairs_end(nwk_ctx *ctx, int32_t *penalties, uint8_t *problem_hash);
 
 /*
  * getMinimumPenalties on a context (skel:117-175, sub:232-364): aligns all
@@ -209,6 +222,22 @@ int nwk_finalize_moves(const uint8_t *x, int32_t m, const uint8_t *y, int32_t n,
 
 /* Chain (skel:159): acc = sha512hex(acc ++ hex(problem_hash[p])), p = 0..P-1. */
 int nwk_chain_hash(const uint8_t *problem_hash, int64_t P, char *hash_hex);
+
+/*
+ * Streaming chain of skel:159 over P pairs, fed in any order as results
+ * arrive (sub:305-337 collects results out of order, then chains): a worker
+ * thread advances the chain over the ready prefix of canonical ids while the
+ * caller works.  feed: n records {pair id, penalty, raw problem hash}, each id
+ * once (penalties may be NULL); finish: waits for the last link and writes
+ * hash_hex[129] and, unless NULL, penalties[P] and problem_hash[P*64] in
+ * canonical order (NWK_EINVAL if some pair was never fed).
+ */
+typedef struct nwk_chain nwk_chain;
+int nwk_chain_create(int64_t P, nwk_chain **out);
+int nwk_chain_feed(nwk_chain *ch, const int64_t *pair_ids, const int32_t *penalties,
+                   const uint8_t *problem_hash, int64_t n);
+int nwk_chain_finish(nwk_chain *ch, char *hash_hex, int32_t *penalties, uint8_t *problem_hash);
+void nwk_chain_destroy(nwk_chain *ch);
 
 /* sw::sha512::calculate equivalent: lowercase hex digest of data[0..len). */
 void nwk_sha512_hex(const uint8_t *data, int64_t len, char *out_hex);

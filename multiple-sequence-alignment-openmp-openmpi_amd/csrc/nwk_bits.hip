@@ -138,10 +138,13 @@ __device__ __forceinline__ void bits_diffs(const unsigned (&X)[NP], const unsign
 //   eh       MASK blocks: this lane's bit-0 column at step s0 (columns < 0 keep
 //            v = 0; strips: the column within the current row pass, so a bit
 //            entering column 0 of its next pass sees the left border)
+//   sto      the block is inside the pair's stored blocks (uniform); lsto: this
+//            lane's words hold a cell of the storage window (bits_lane_stored)
 template <int NP, int SR, bool MASK, bool PROD>
 __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsigned x1, unsigned yp0, unsigned yp1,
                                            unsigned w0, unsigned w1, unsigned (&H)[NP], unsigned (&V)[NP],
-                                           const unsigned* cons, unsigned* ring, unsigned* st, bool sto, int eh) {
+                                           const unsigned* cons, unsigned* ring, unsigned* st, bool sto, int eh,
+                                           bool lsto) {
   unsigned dw[8], uw[8];
   // the band-above entries are read one step ahead (an LDS read's latency
   // would otherwise sit on every step's dependence chain)
@@ -236,10 +239,25 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
   return;
 #endif
   if (!sto) return;  // block outside the pair's stored window (PairDesc::bits_w)
+  if (!lsto) return;  // (per lane: the active lanes are contiguous, so the stores stay whole lines)
   __builtin_nontemporal_store(u4{dw[0], dw[1], dw[2], dw[3]}, reinterpret_cast<u4*>(st));
   __builtin_nontemporal_store(u4{dw[4], dw[5], dw[6], dw[7]}, reinterpret_cast<u4*>(st + 256));
   __builtin_nontemporal_store(u4{uw[0], uw[1], uw[2], uw[3]}, reinterpret_cast<u4*>(st + 512));
   __builtin_nontemporal_store(u4{uw[4], uw[5], uw[6], uw[7]}, reinterpret_cast<u4*>(st + 768));
+}
+
+// Windowed storage writes only the lane words that hold a cell within w
+// columns of the diagonal: lane words of one 8-step block cover rows R .. R+31
+// (R = the lane's bit-0 row) at columns e - b (e = bit 0's column, b = bit), so
+// dev = c m - i n over them spans [(e - 31) m - (R + 31) n, (e + 7) m - R n]
+// (e at the block's first step).  hi = (e + 7) m - R n; the words are kept iff
+// that span meets [-w m, w m].  The trace checks every cell it reads against
+// the same |dev| <= w m (a kept cell's words were written) and flags the pair
+// for a full re-run when its path leaves.  With w >= 2048 rows' worth this
+// keeps nearly every word; at C4's w = 1024 about half of them, which halves
+// the HBM writes of the stored blocks.
+__device__ __forceinline__ bool bits_lane_stored(int64_t hi, int64_t lim, int64_t span) {
+  return hi >= -lim && hi - span <= lim;
 }
 
 // Traceback of one pair from (m, n) over the stored (diag, up) bits.  A tile
@@ -254,17 +272,17 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
 #ifndef NWK_TRACE_PRIO
 #define NWK_TRACE_PRIO 0
 #endif
-// NWK_TRACE_MASKS 1: a branch-free walk on per-row ballot masks (SGPR bit tests)
-// instead of two v_readlane per move.  Measured equal (C3 8-rank shard: 9.7-10.0
-// vs 9.5 ms per 100k-move trace: a lone wave issues about one instruction per
-// 4 cycles, so ~50 instructions per move bound either walk), so 0 stays.
-#ifndef NWK_TRACE_MASKS
-#define NWK_TRACE_MASKS 0
-#endif
 __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd, unsigned char* obuf, int lane,
                                            unsigned* prog) {
   const int nblk = pd.bits_nblk, win = pd.bits_w;
   const int64_t bdw = (int64_t)nblk * 1024;  // dwords per band
+  // Storage map.  Banded tasks: band b's step s = c + r (its own numbering),
+  // stored blocks bits_blk_lo(b) .. + nblk at b * bdw.  Strips (pd.bits_np =
+  // n' > 0, one wave sweeps every band): s = c + r + b n' (the strip's
+  // numbering); windowed, band b keeps blocks strip_blk_lo(b) .. + nblk at
+  // b * bdw; full storage is one region of nblk blocks from block 0.
+  const int snp = pd.bits_np;
+  const bool sfull = snp > 0 && win <= 0;
   const unsigned* mat = a.mat + pd.mat_off;
   uint8_t* ops = a.ops + pd.ops_off;
   const unsigned ob = (unsigned)(uintptr_t)obuf;
@@ -285,15 +303,21 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
   int tb = -1, ts = 0, tt = 0, blo = 0, slo = 0;
   unsigned vd0 = 0, vu0 = 0, vd1 = 0, vu1 = 0;
   bool bad = false, out = false;
-  while (c >= 0 && (b > 0 || r >= 0)) {
+  // windowed storage keeps only the lane words holding a cell within win
+  // columns of the diagonal (bits_lane_stored): dev = c m - i n of the current
+  // cell (i = b 2048 + r), |dev| <= win m, else the path has left them
+  int64_t dev = (int64_t)c * pd.m - (int64_t)(b * kBR + r) * pd.n;
+  const int64_t lim = (int64_t)win * pd.m, dD = (int64_t)pd.n - pd.m;
+  if (win > 0 && c >= 0 && (dev > lim || dev < -lim)) out = true;
+  while (!out && c >= 0 && (b > 0 || r >= 0)) {
     if (r < 0) {  // into the band above
       --b;
       r += kBR;
     }
     int t = r >> 5;
-    int s = c + r;
+    int s = c + r + (snp > 0 ? b * snp : 0);
     if (b != tb) {
-      blo = bits_blk_lo(b, pd.m, pd.n, win);
+      blo = snp > 0 ? strip_blk_lo(b, pd.m, pd.n, snp, win) : bits_blk_lo(b, pd.m, pd.n, win);
       slo = 8 * blo;  // lowest stored step of band b
     }
     if ((unsigned)((s >> 3) - blo) >= (unsigned)nblk) {  // the path left the stored window
@@ -309,8 +333,8 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
       const int rel = (sl >> 3) - blo;
       vd0 = vu0 = vd1 = vu1 = 0;
       if (sl >= 0 && (unsigned)rel < (unsigned)nblk) {
-        const unsigned* p0 =
-            mat + (int64_t)b * bdw + (int64_t)rel * 1024 + ((sl & 7) >> 2) * 256 + t * 4 + (sl & 3);
+        const unsigned* p0 = mat + (sfull ? 0 : (int64_t)b * bdw) + (int64_t)rel * 1024 + ((sl & 7) >> 2) * 256 +
+                             t * 4 + (sl & 3);
         vd0 = __builtin_nontemporal_load(p0);
         vu0 = __builtin_nontemporal_load(p0 + 512);
         if (t > 0) {
@@ -320,44 +344,11 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
       }
     }
     // walk inside the tile
-#if NWK_TRACE_MASKS
-    // Row masks: bit l of Dr / Ur = the diag / up bit of row r at step ts - l
-    // (one ballot each).  Every D or U move goes to row r - 1, so its masks
-    // are built one move ahead and the decisions are scalar bit tests on
-    // SGPRs; only the ballots (off the decision chain) and the move's LDS
-    // write touch the VALU.
-    auto row_masks = [&](int x, u64& dm, u64& um) {
-      const bool h = (x >> 5) == tt;
-      const unsigned sh = (unsigned)(x & 31);
-      dm = __builtin_amdgcn_ballot_w64((((h ? vd0 : vd1) >> sh) & 1u) != 0u);
-      um = __builtin_amdgcn_ballot_w64((((h ? vu0 : vu1) >> sh) & 1u) != 0u);
-    };
-    u64 Dr, Ur, Dn, Un;
-    row_masks(r, Dr, Ur);
-    row_masks(r - 1, Dn, Un);  // (rows outside the tile: junk, never read -- the walk leaves first)
-    int L = ts - s;
-    const int rlo = 32 * (tt - 1);  // lowest row of the tile
     for (;;) {
-      // branch-free move: D (diag bit), else U (up bit clear), else L
-      const unsigned isD = (unsigned)(Dr >> L) & 1u;
-      const unsigned isU = ~isD & ~(unsigned)(Ur >> L) & 1u;
-      const unsigned down = isD | isU;  // row r - 1 next
-      const unsigned op = isD ? 'D' : isU ? 'U' : 'L';
-      asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(op) : "memory");
-      ++Lc;
-      r -= (int)down;
-      c -= (int)(isD | (down ^ 1u));
-      L += 1 + (int)isD;
-      Dr = down ? Dn : Dr;
-      Ur = down ? Un : Ur;
-      if (Lc - flushed >= 192) flush(Lc & ~3);
-      if ((c | r) < 0 || L >= 64 || r < rlo || ts - L < slo) break;
-      row_masks(r - 1, Dn, Un);
-    }
-    t = r >> 5;
-    s = ts - L;
-#else
-    for (;;) {
+      if (win > 0 && (dev > lim || dev < -lim)) {  // this cell is outside the stored lane words
+        out = true;
+        break;
+      }
       // straight-line uniform code: one select per word, one v_readlane each
       const int L = __builtin_amdgcn_readfirstlane(ts - s);
       const bool hi = __builtin_amdgcn_readfirstlane(t - tt) == 0;
@@ -371,14 +362,17 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
         --r;
         --c;
         s -= 2;
+        dev += dD;
       } else if (!((u >> bit) & 1u)) {  // up: v == 0 (the stored word is v's plane 0)
         op = 'U';
         --r;
         s -= 1;
+        dev += pd.n;
       } else {
         op = 'L';
         --c;
         s -= 1;
+        dev -= pd.m;
       }
       asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(op) : "memory");
       ++Lc;
@@ -387,7 +381,7 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
       t = r >> 5;
       if (s <= ts - 64 || (t != tt && t != tt - 1) || s < slo) break;
     }
-#endif
+    if (out) break;
     if (Lc > pd.m + pd.n) {
       bad = true;
       break;
@@ -465,6 +459,10 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
     u64* gout = a.bnd + pd.bnd_off + (int64_t)band * nch * NG;
     const int nblk = pd.bits_nblk, blo = bits_blk_lo(band, pd.m, pd.n, pd.bits_w);
     unsigned* mb = a.mat + pd.mat_off + (int64_t)band * nblk * 1024 + lane * 4;
+    // windowed: per-lane store predicate (bits_lane_stored) for rows R0 + 32 lane ..
+    const bool lwin = pd.bits_w > 0;
+    const int64_t lim = (int64_t)pd.bits_w * pd.m, span = 38ll * pd.m + 31ll * pd.n;
+    const int64_t negRn = -(int64_t)(R0 + 32 * lane) * pd.n;
     // y windows: lane t's window for the half starting at step s_h is position s_h - 32 t
     const unsigned* ywp = a.yw + 2 * (pd.e_off - 32 * (int64_t)lane);
     unsigned yp0 = 0, yp1 = 0;
@@ -523,12 +521,13 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
         const bool sto = (unsigned)rel < (unsigned)nblk;
         unsigned* st = mb + (int64_t)rel * 1024;
         const int eh = s0 - 32 * lane;
+        const bool ls = !lwin || bits_lane_stored((int64_t)(eh + 7) * pd.m + negRn, lim, span);
         if (mask) {
-          if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh);
-          else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh);
+          if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
+          else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
         } else {
-          if (prod) bits_block<NP, SR, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh);
-          else bits_block<NP, SR, false, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh);
+          if (prod) bits_block<NP, SR, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
+          else bits_block<NP, SR, false, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
         }
         if ((blk & 3) == 3) {  // end of a 32-step half: its window becomes the previous one
           yp0 = w0;
@@ -588,10 +587,211 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
   }
 }
 
+// Rolling strips (mode kBitsStrip): one wave sweeps ALL bands of a pair.
+// Lane bit p (= 32 lane + b) runs rows p, p + 2048, p + 4096, ... : at step s
+// its virtual column is v = s - p, its row pass k = v / n' and its column
+// v % n' (n' = a multiple of 64, at least n + 32: the 32+ columns past n are
+// junk).  When a bit leaves its pass it enters column 0 of row p + 2048 (k + 1):
+//   * its left input must be the border (v = 0): the MASK blocks clear V of
+//     the bits that have not yet entered the pass, as the banded kernel does
+//     for columns < 0 -- those bits are in the junk columns of the pass before;
+//   * its row code changes: a lane switches x to its next pass's rows at the
+//     32-step half where its bit 0 enters the pass (its bits 1..31 are still
+//     in junk columns, so their codes do not matter);
+//   * lane 0 bit 0 (row 2048 (k + 1)) reads the pass above's last row (lane
+//     63 bit 31, row 2048 k + 2047) -- produced by this same wave n' - 2047
+//     steps earlier, so it goes through an LDS ring of one 64-column chunk per
+//     slot (hand[], 2 NP packed dwords per chunk) instead of HBM granules, and
+//     nothing ever waits.
+// Against 2048-row band tasks (each band sweeps n + 2048 steps, the skew paid
+// per band) a strip pays the 2047-step skew once per pair, and it needs no
+// inter-wave hand-off.  The price is the pair's latency (one wave does all
+// nb x n' steps), so the runtime picks strips for jobs with many pairs per
+// wave slot (C4: 32,640 pairs of 8k on 4,096 slots).
+// y windows: the column sequence's usual windows, indexed by the wrapped
+// column (32-step halves are 32-aligned and n' is a multiple of 64, so a
+// window never straddles the wrap).  Row codes: the row sequence's y windows,
+// bit-reversed (bit b = row 32 lane + b).  Storage: the strip's 8-step blocks
+// in order (full), or per band the blocks strip_blk_lo(band) .. + nblk of its
+// W-column diagonal window (the runtime keeps the bands' windows disjoint).
+template <int NP, int SR>
+__global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned cons_all[4][64 * NP];
+  __shared__ __attribute__((aligned(16))) unsigned ring_all[4][128 * NP];
+  __shared__ __attribute__((aligned(16))) unsigned char obuf_all[4][256];
+  extern __shared__ __attribute__((aligned(16))) unsigned hand_all[];  // [4][a.strip_ring]
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  unsigned* prog = a.prog ? a.prog + blockIdx.x * 4 + wid : nullptr;  // NWK_WATCHDOG markers
+  unsigned* cons = cons_all[wid];
+  unsigned* ring = ring_all[wid];
+  unsigned* hand = hand_all + wid * a.strip_ring;
+  constexpr int NG = 2 * NP;  // packed dwords per 64-column chunk of a pass's last row
+
+  for (;;) {
+    unsigned tk = 0;
+    if (lane == 0) tk = atomicAdd(a.counter, 1u);
+    tk = __builtin_amdgcn_readfirstlane(tk);
+    BITS_PROG(0x10000000u | tk);
+    if (tk >= (unsigned)a.ntasks) { BITS_PROG(0x60000000u); return; }
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)a.err, BITS_RLX)) != 0u) return;
+    const PairDesc pd = a.pairs[a.tasks[tk].x];
+    const int np = pd.bits_np, nch = np >> 6, nb = pd.nbands, nsb = pd.sblocks;
+    if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 6] = __builtin_amdgcn_s_memrealtime();
+    // row code planes of pass 0 and (ahead) pass 1: bit b = row 2048 k + 32 lane + b
+    const unsigned* xw = a.yw + 2 * (pd.xw_off + 32 * (int64_t)lane);
+    unsigned x0 = __builtin_bitreverse32(xw[0]), x1 = __builtin_bitreverse32(xw[1]);
+    unsigned nx0 = 0, nx1 = 0;
+    if (nb > 1) {
+      nx0 = __builtin_bitreverse32(xw[2 * kBR]);
+      nx1 = __builtin_bitreverse32(xw[2 * kBR + 1]);
+    }
+    unsigned H[NP], V[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) H[k] = V[k] = 0u;
+    // y windows by wrapped column: ua / ub = this lane's bit-0 column at the
+    // start of the super-block's two halves (negative before pass 0 starts)
+    const unsigned* yb = a.yw + 2 * pd.e_off;
+    int ua = -32 * lane, ub = ua + 32;
+    unsigned wa0 = yb[2 * ua], wa1 = yb[2 * ua + 1], wb0 = yb[2 * ub], wb1 = yb[2 * ub + 1];
+    unsigned yp0 = 0, yp1 = 0;
+    const bool win = pd.bits_w > 0;
+    const int nblk = pd.bits_nblk;
+    int kw = 0, blo = win ? strip_blk_lo(0, pd.m, pd.n, np, pd.bits_w) : 0;  // current storage window
+    // per-lane store predicate (bits_lane_stored) for the rows of the lane's current pass
+    const int64_t lim = (int64_t)pd.bits_w * pd.m, span = 38ll * pd.m + 31ll * pd.n;
+    int64_t negRn = -(int64_t)(32 * lane) * pd.n;
+    unsigned* mb = a.mat + pd.mat_off + lane * 4;
+    int q0 = 0, k0 = 0;  // lane 0 bit 0: chunk and pass of this super-block
+    int pslot = 0;       // hand[] slot of the chunk published at the end of this super-block (sb >= 32)
+
+    for (int sb = 0; sb < nsb; ++sb) {
+      BITS_PROG(0x20000000u | (unsigned)sb);
+      // --- pass k0's row above (pass k0 - 1's last row) for columns 64 q0 .. + 63 -> cons
+      if (k0 > 0) {
+        const unsigned dat = lane < NG ? hand[q0 * NG + lane] : 0u;
+        unsigned e[NP];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+          const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)dat, 2 * k);
+          const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)dat, 2 * k + 1);
+          const unsigned w = lane < 32 ? lo : hi;
+          e[k] = (w >> (lane & 31)) << 31;
+        }
+        if constexpr (NP == 4) *reinterpret_cast<uint4*>(cons + lane * 4) = make_uint4(e[0], e[1], e[2], e[3]);
+        else *reinterpret_cast<uint2*>(cons + lane * 2) = make_uint2(e[0], e[1]);
+      } else if (sb == 0) {  // pass 0: the top border (zeros)
+        if constexpr (NP == 4) *reinterpret_cast<uint4*>(cons + lane * 4) = make_uint4(0, 0, 0, 0);
+        else *reinterpret_cast<uint2*>(cons + lane * 2) = make_uint2(0, 0);
+      }
+      // next super-block's windows (wrapped), and ahead of a pass boundary the
+      // next pass's row codes (lane t switches to them t / 2 super-blocks later)
+      int na = ua + 64;
+      if (na >= np) na -= np;
+      int nbw = na + 32;
+      if (nbw >= np) nbw -= np;
+      const unsigned na0 = yb[2 * na], na1 = yb[2 * na + 1], nb0 = yb[2 * nbw], nb1 = yb[2 * nbw + 1];
+      if (q0 == nch - 1 && k0 > 0 && k0 + 1 < nb) {  // (pass 1's codes were loaded with the task)
+        nx0 = __builtin_bitreverse32(xw[2 * (int64_t)kBR * (k0 + 1)]);
+        nx1 = __builtin_bitreverse32(xw[2 * (int64_t)kBR * (k0 + 1) + 1]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+
+      const bool mask = q0 < 32;  // some lane's bit 0 enters a pass in this super-block
+      const bool prod = sb >= 31;
+#pragma unroll
+      for (int blk = 0; blk < 8; ++blk) {
+        const int s0 = 64 * sb + 8 * blk;
+        const unsigned w0 = blk < 4 ? wa0 : wb0, w1 = blk < 4 ? wa1 : wb1;
+        const int uh = blk < 4 ? ua : ub;
+        if ((blk & 3) == 0 && mask) {  // this lane's bit 0 enters pass >= 1 here: switch the row codes
+          const bool sw = uh == 0 && s0 > 32 * lane;
+          x0 = sw ? nx0 : x0;
+          x1 = sw ? nx1 : x1;
+          negRn -= sw ? (int64_t)kBR * pd.n : 0;
+        }
+        const int eh = uh + 8 * (blk & 3);
+        const int K = 8 * sb + blk;  // the block's index in the strip
+        bool sto = true;
+        unsigned* st = mb + (int64_t)K * 1024;
+        if (win) {
+          while (kw < nb && K >= blo + nblk) {
+            ++kw;
+            blo = kw < nb ? strip_blk_lo(kw, pd.m, pd.n, np, pd.bits_w) : 0;
+          }
+          sto = kw < nb && K >= blo;
+          st = mb + ((int64_t)kw * nblk + (K - blo)) * 1024;
+        }
+        const bool ls = !win || bits_lane_stored((int64_t)(eh + 7) * pd.m + negRn, lim, span);
+        if (mask) {
+          if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
+          else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
+        } else {
+          if (prod) bits_block<NP, SR, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
+          else bits_block<NP, SR, false, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
+        }
+        if ((blk & 3) == 3) {  // end of a 32-step half: its window becomes the previous one
+          yp0 = w0;
+          yp1 = w1;
+        }
+      }
+      wa0 = na0; wa1 = na1; wb0 = nb0; wb1 = nb1;
+      ua = na;
+      ub = nbw;
+      // --- chunk sb - 32 of the strip's last-row stream (lane 63 bit 31) is complete: into hand[]
+      if (sb >= 32) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const unsigned* e = ring + ((64 * sb + lane) & 127) * NP;
+        unsigned val = 0;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+          const u64 m64 = __ballot((e[k] >> 31) != 0u);
+          val = lane == 2 * k ? (unsigned)m64 : val;
+          val = lane == 2 * k + 1 ? (unsigned)(m64 >> 32) : val;
+        }
+        if (lane < NG) hand[pslot * NG + lane] = val;
+        if (++pslot == nch) pslot = 0;
+      }
+      if (++q0 == nch) {
+        q0 = 0;
+        ++k0;
+      }
+    }
+    BITS_PROG(0x30000000u);
+    // the trace reads this wave's own stores
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
+    BITS_PROG(0x40000000u);
+    trace_bits(a, pd, obuf_all[wid], lane, prog);
+    if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
+    BITS_PROG(0x56000000u);
+  }
+}
+
 template <int NP, int SR>
 hipError_t bits_launch(const FillArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL((nw_align_bits<NP, SR>), dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
+}
+
+template <int NP, int SR>
+hipError_t strip_launch(const FillArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((nw_align_strip<NP, SR>), dim3(grid), dim3(256), (size_t)4 * a.strip_ring * 4, s, a);
+  return hipGetLastError();
+}
+
+template <int NP, int SR>
+int strip_occ(int ring_dwords) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&nw_align_strip<NP, SR>), 256,
+                                                   (size_t)4 * ring_dwords * 4) != hipSuccess)
+    return 1;
+  return n > 0 ? n : 1;
 }
 
 template <int NP, int SR>
@@ -637,5 +837,32 @@ hipError_t launch_bits(const FillArgs& a, int pxy, int pgap, int grid, hipStream
 }
 
 int bits_blocks_per_cu(int pgap) { return pgap == 1 ? bits_occ<2, 1>() : bits_occ<4, 1>(); }
+
+hipError_t launch_strip(const FillArgs& a, int pxy, int pgap, int grid, hipStream_t s) {
+  const int sr = bits_sr(pxy, pgap);
+  if (pgap == 1) {
+    switch (sr) {
+      case -1: return strip_launch<2, -1>(a, grid, s);
+      case 0: return strip_launch<2, 0>(a, grid, s);
+      case 1: return strip_launch<2, 1>(a, grid, s);
+      default: return strip_launch<2, 2>(a, grid, s);
+    }
+  }
+  if (pgap == 2) {
+    switch (sr) {
+      case -1: return strip_launch<4, -1>(a, grid, s);
+      case 0: return strip_launch<4, 0>(a, grid, s);
+      case 1: return strip_launch<4, 1>(a, grid, s);
+      case 2: return strip_launch<4, 2>(a, grid, s);
+      case 3: return strip_launch<4, 3>(a, grid, s);
+      default: return strip_launch<4, 4>(a, grid, s);
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+int strip_blocks_per_cu(int pgap, int ring_dwords) {
+  return pgap == 1 ? strip_occ<2, 1>(ring_dwords) : strip_occ<4, 1>(ring_dwords);
+}
 
 }  // namespace nwk

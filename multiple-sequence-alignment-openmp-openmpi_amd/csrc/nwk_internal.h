@@ -27,6 +27,7 @@ enum Mode : int {
   kProfileDP = 6,  // profile-profile sum-of-pairs DP of the progressive MSA, 4-bit codes
   kAffinePk = 7,   // kAffine on band pairs as int16 pairs (nw_align_pka), layout LY 2, profile codes
   kBits = 8,       // bit-sliced difference planes (nw_align_bits, nwk_bits.hip): 2048-row bands, 2-bit traceback
+  kBitsStrip = 9,  // kBits as rolling strips (nw_align_strip): one wave per pair, every band in turn
 };
 constexpr int kBitsRows = 2048;  // kBits: rows per band (64 lanes x 32 bits)
 
@@ -60,12 +61,26 @@ struct PairDesc {
   // bits_blk_lo(b) ..); kAffinePk: bits_nblk 64-step super-blocks per band
   // pair (band pair p keeps super-blocks pka_sb_lo(p) ..).
   int32_t bits_w, bits_nblk;
+  // kBitsStrip: columns per row pass n' (a multiple of 64, >= n + 32): one
+  // wave sweeps all bands of the pair as a rolling 2048-row strip -- lane bit p
+  // runs rows p, p + 2048, ... with virtual column v = s - p, pass v / n',
+  // column v % n' (0 = banded tasks)
+  int32_t bits_np, pad_;
+  int64_t xw_off;   // kBitsStrip: y-window index of the row sequence's position 0 (its row codes)
 };
 
 // kBits: first stored 8-step block of band b (see PairDesc::bits_w)
 __host__ __device__ inline int bits_blk_lo(int b, int m, int n, int w) {
   if (w <= 0) return 0;
   const int64_t lo = (int64_t)b * kBitsRows * n / m - w;
+  return lo <= 0 ? 0 : (int)(lo >> 3);
+}
+
+// kBitsStrip: first stored 8-step block (strip step numbering) of band b's
+// window: its cells (i, j), |j - i n / m| <= w, sit at steps j + b np + (i - 2048 b)
+__host__ __device__ inline int strip_blk_lo(int b, int m, int n, int np, int w) {
+  if (w <= 0) return 0;
+  const int64_t lo = (int64_t)b * np + (int64_t)b * kBitsRows * n / m - w;
   return lo <= 0 ? 0 : (int)(lo >> 3);
 }
 
@@ -114,6 +129,7 @@ struct FillArgs {
   const int* pcol;         // kProfileDP: per Y column (DP column) 8 ints {cnt[0..5], gy, H[0][j]} at pairs[].y_off
   const unsigned* yw;      // kBits: per y position p two dwords (code bit planes of y[p .. p+31], y[p] at bit 31), at pairs[].e_off
   int* retry;              // windowed storage: per slot, 1 = the path left the stored window (re-run in full)
+  int strip_ring;          // kBitsStrip: LDS dwords per wave of the hand-off ring (max n' / 64 x 2 NP)
 };
 constexpr int kProfSyms = 6;  // kProfileDP: symbols + gap per column profile
 
@@ -144,6 +160,8 @@ int fill_blocks_per_cu(int mode, int bits);
 bool bits_admissible(int pxy, int pgap, int alpha);
 hipError_t launch_bits(const FillArgs& a, int pxy, int pgap, int grid, hipStream_t s);
 int bits_blocks_per_cu(int pgap);
+hipError_t launch_strip(const FillArgs& a, int pxy, int pgap, int grid, hipStream_t s);
+int strip_blocks_per_cu(int pgap, int ring_dwords);
 
 // Dwords of one band of the stored matrix.
 __host__ __device__ inline int64_t band_dwords(int bits, int sblocks) {

@@ -15,6 +15,8 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -178,6 +180,15 @@ struct nwk_ctx {
   HostBuf h_retry;  // kBits windowed storage: per slot of the last batch, 1 = re-run with full storage
 
   nwk_stats stats{};
+
+  // nwk_align_pairs_begin / _end: one call in flight on a host thread
+  std::thread async;
+  bool pending = false;
+  std::vector<int64_t> a_ids;
+  std::vector<int32_t> a_pen;
+  std::vector<uint8_t> a_hash;
+  int a_rc = NWK_OK;
+  std::string a_err;
 };
 
 extern "C" {
@@ -198,6 +209,7 @@ int nwk_device_count(void) {
 
 void nwk_ctx_destroy(nwk_ctx* c) {
   if (!c) return;
+  if (c->async.joinable()) c->async.join();
   (void)hipSetDevice(c->device);
   for (auto& b : c->d_codes) b.release();
   for (auto& b : c->d_E) b.release();
@@ -229,7 +241,7 @@ int nwk_ctx_create(const nwk_opts* opts, nwk_ctx** out) {
   if (const char* v = getenv("NWK_VERBOSE")) o.verbose = atoi(v);  // debug: diagnostics on stderr
   // option checks first: they need no device
   if (o.finalize < 0 || o.finalize > 2) return fail(NWK_EINVAL, "nwk_ctx_create: finalize must be 0/1/2");
-  if (o.kernel < 0 || o.kernel > 4) return fail(NWK_EINVAL, "nwk_ctx_create: kernel must be 0..4");
+  if (o.kernel < 0 || o.kernel > 5) return fail(NWK_EINVAL, "nwk_ctx_create: kernel must be 0..5");
   if (o.bits != 0 && o.bits != 4 && o.bits != 8 && o.bits != 16 && o.bits != 32)
     return fail(NWK_EINVAL, "nwk_ctx_create: bits must be 0/4/8/16/32");
   if (ndev <= 0) return fail(NWK_EDEVICE, "nwk_ctx_create: no HIP device visible");
@@ -470,7 +482,7 @@ int choose_plan(const nwk_ctx* c, const Scoring& sc, Plan* pl) {
   // driver's NWK_BITS is the storage width, opts.bits).
   // pl->bits keeps the profile kernels' width (the linear-space path uses it).
   static const int bits_env = getenv("NWK_BITS_KERNEL") ? atoi(getenv("NWK_BITS_KERNEL")) : 1;
-  const bool want_bits = c->opts.kernel == 4 || (c->opts.kernel == 0 && bits_env != 0);
+  const bool want_bits = c->opts.kernel == 4 || c->opts.kernel == 5 || (c->opts.kernel == 0 && bits_env != 0);
   if (want_bits && c->opts.bits == 0 && bits_admissible(pxy, pgap, c->alpha)) pl->mode = kBits;
   return NWK_OK;
 }
@@ -480,7 +492,7 @@ int choose_plan(const nwk_ctx* c, const Scoring& sc, Plan* pl) {
 inline bool band_pairs(int mode) { return mode == kPacked2 || mode == kAffinePk; }
 inline int sblocks_of(int mode, int64_t nch) { return (int)(nch + (mode == kPacked || band_pairs(mode) ? 2 : 1)); }
 // Fill tasks per pair: bands, or band pairs (kPacked2, kAffinePk).
-inline int64_t tasks_of(int mode, int64_t nb) { return band_pairs(mode) ? (nb + 1) / 2 : nb; }
+inline int64_t tasks_of(int mode, int64_t nb) { return mode == kBitsStrip ? 1 : band_pairs(mode) ? (nb + 1) / 2 : nb; }
 
 // kPacked2 segmented traceback footprint for a speculative segment every E
 // tasks (E = 0: one whole-pair segment): move buffers (segment k starts on
@@ -515,6 +527,48 @@ int64_t bits_nblk_of(int m, int n, int w) {
   return std::min(all, ceil_div(width, 8) + 1);
 }
 
+// kBitsStrip geometry (nw_align_strip, nwk_bits.hip): n' = columns per row
+// pass, a multiple of 64 with >= 32 junk columns past n (the wrap's masked
+// bits sit there); the strip runs until row m - 1 reaches column n - 1.
+inline int strip_np(int n) { return (int)round_up((int64_t)n + 32, 64); }
+inline int strip_sblocks(int m, int n) {
+  const int np = strip_np(n), nb = (int)ceil_div(m, kBitsRows);
+  const int64_t last = (int64_t)(nb - 1) * np + (n - 1) + (m - (int64_t)kBitsRows * (nb - 1) - 1);
+  return (int)(last / 64 + 1);
+}
+// LDS hand-off ring per wave (dwords): one 64-column chunk of a pass's last row
+// per slot, 2 NP packed dwords each; at most kStripMaxChunks chunks keeps 4
+// workgroups (16 waves) per CU; at least 64 chunks keeps the hand-off's lag
+// (n' / 64 - 32 super-blocks) and the lanes' 32-super-block pass entry apart
+constexpr int kStripMinChunks = 64;
+inline int strip_max_chunks(int pgap) { return pgap == 1 ? 500 : 200; }
+inline bool strip_admissible(int m, int n, int pgap) {
+  const int nch = strip_np(n) / 64;
+  return m > 0 && n > 0 && nch >= kStripMinChunks && nch <= strip_max_chunks(pgap);
+}
+// stored 8-step blocks: full (the whole strip) or, windowed, per band; the
+// bands' windows must not overlap (a block is stored into one window only) --
+// a pair whose windows would overlap keeps full storage
+void strip_storage(PairWork* w) {
+  const int np = strip_np(w->n), nb = (int)ceil_div(w->m, kBitsRows);
+  const int64_t full = 8 * (int64_t)strip_sblocks(w->m, w->n);
+  if (w->bits_w > 0) {
+    const int64_t width = (kBitsRows - 1) + ceil_div((int64_t)(kBitsRows - 1) * w->n, w->m) + 2 * (int64_t)w->bits_w + 16;
+    const int64_t nblk = ceil_div(width, 8) + 1;
+    bool ok = nb * nblk < full;
+    for (int k = 0; ok && k + 1 < nb; ++k)
+      ok = strip_blk_lo(k + 1, w->m, w->n, np, w->bits_w) >= strip_blk_lo(k, w->m, w->n, np, w->bits_w) + nblk;
+    if (ok) {
+      w->bits_nblk = (int)nblk;
+      w->mat_dw = nb * nblk * 1024;
+      return;
+    }
+    w->bits_w = 0;
+  }
+  w->bits_nblk = (int)full;
+  w->mat_dw = full * 1024;
+}
+
 // kAffinePk stored super-blocks per band pair (bits_w > 0): pka_sb_lo(p) lies
 // at or below the steps of its rows' window cells (>= R n / m - w - 1) and the
 // highest is below (R + 1024) n / m + w + 127 (lane 63, the odd band's skew)
@@ -542,6 +596,14 @@ int choose_window(int mode, int batches, int64_t budget, Need&& need) {
 }
 
 void footprint(PairWork* w, int bits, int mode, bool affine) {
+  if (mode == kBitsStrip) {
+    w->segops_b = w->segctl_b = 0;
+    w->spec = 0;
+    strip_storage(w);
+    w->bnd_gr = 0;  // the pass-to-pass hand-off stays in LDS
+    w->ops_b = round_up((int64_t)w->m + w->n, 16);
+    return;
+  }
   if (mode == kBits) {
     const int64_t nb = ceil_div(w->m, kBitsRows), nch = ceil_div(w->n, 64);
     w->segops_b = w->segctl_b = 0;
@@ -655,18 +717,20 @@ struct Chain {
   const uint8_t* hashes = nullptr;  // [P][64] raw problem hashes
   std::vector<char> ready;
   int64_t next = 0;
-  char buf[256];
-  size_t la = 0;  // acc starts as "" (skel:121)
+  ChainAcc acc;  // acc starts as "" (skel:121)
   void advance() {
     const int64_t P = (int64_t)ready.size();
+    uint64_t kw[80];
     while (next < P && ready[next]) {
-      to_hex(hashes + 64 * next, buf + la);
-      char acc[128];
-      sha512_hex(buf, la + 128, acc);
-      memcpy(buf, acc, 128);
-      la = 128;
+      chain_schedule(hashes + 64 * next, kw);
+      chain_step(&acc, kw);
       ++next;
     }
+  }
+  // hash_hex[129]: the answer ("" for no pairs)
+  void hex(char* out) const {
+    chain_hex(acc, out);
+    out[acc.empty ? 0 : 128] = 0;
   }
 };
 
@@ -703,7 +767,8 @@ LinGeo lin_geo(const Plan& pl, const PairWork& w, int G) {
 
 Plan lin_plan(const Plan& pl0) {
   Plan pl = pl0;
-  if (pl.mode == kPacked || pl.mode == kPacked2 || pl.mode == kBits) pl.mode = kProfile;  // same bits, codes, K0/K1
+  if (pl.mode == kPacked || pl.mode == kPacked2 || pl.mode == kBits || pl.mode == kBitsStrip)
+    pl.mode = kProfile;  // same bits, codes, K0/K1
   return pl;
 }
 
@@ -872,6 +937,49 @@ int align_linear_batch(nwk_ctx* c, const Plan& pl0, const Scoring& sc, const Pai
   return NWK_OK;
 }
 
+// Strips or band tasks for a kBits job (nw_align_strip vs nw_align_bits).  A
+// strip sweeps all of a pair's bands in one wave: fewer steps (the 2047-step
+// skew once per pair, not per band: ~16% on 8k pairs) and no inter-wave
+// hand-off, but the pair's latency is its whole strip.  Estimated makespans
+// in wave-steps: band tasks max(total band steps / slots, the longest pair's
+// pipeline n + nb x 2112); strips the LPT list schedule of the strip lengths
+// over the wave slots.  force: 1 = strips wherever admissible (tests).
+bool use_strips(const nwk_ctx* c, const std::vector<PairWork>& work, int pgap, bool force, int* ring_out) {
+  int ring = 0;
+  int64_t npairs = 0;
+  for (const auto& w : work) {
+    if (w.m == 0 || w.n == 0) continue;
+    if (!strip_admissible(w.m, w.n, pgap)) return false;
+    ring = std::max(ring, strip_np(w.n) / 64 * 4 * pgap);
+    ++npairs;
+  }
+  *ring_out = ring;
+  if (npairs == 0) return false;
+  if (force) return true;
+  const int64_t slots_b = 4LL * bits_blocks_per_cu(pgap) * c->cus;
+  const int64_t slots_s = 4LL * strip_blocks_per_cu(pgap, ring) * c->cus;
+  double band_steps = 0, span = 0;
+  std::vector<int64_t> len;
+  len.reserve((size_t)npairs);
+  for (const auto& w : work) {
+    if (w.m == 0 || w.n == 0) continue;
+    const int64_t nb = ceil_div(w.m, kBitsRows), nch = ceil_div(w.n, 64);
+    band_steps += (double)nb * (nch + 32) * 64;
+    span = std::max(span, (double)w.n + nb * (kBitsRows + 64.0));
+    len.push_back(64LL * strip_sblocks(w.m, w.n));
+  }
+  const double est_b = std::max(band_steps / (double)slots_b, span);
+  std::sort(len.begin(), len.end(), std::greater<int64_t>());
+  std::vector<int64_t> heap((size_t)std::min<int64_t>(slots_s, npairs), 0);  // min-heap of slot finish times
+  for (int64_t L : len) {
+    std::pop_heap(heap.begin(), heap.end(), std::greater<int64_t>());
+    heap.back() += L;
+    std::push_heap(heap.begin(), heap.end(), std::greater<int64_t>());
+  }
+  const double est_s = (double)*std::max_element(heap.begin(), heap.end());
+  return est_s < 0.95 * est_b;
+}
+
 int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32_t* penalties,
                uint8_t* hashes, std::vector<uint8_t>* a1, std::vector<uint8_t>* a2, Chain* chain = nullptr) {
   const double t_start = now_ms();
@@ -896,7 +1004,16 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       if (w.m > 0 && w.n > 0) t2 += ceil_div(w.m, 2 * kBandRows);
     if (t2 < 8 * (int64_t)c->cus) pl.mode = kPacked;  // (2048 on 256 CUs; the kernels tie near there)
   }
-  st.bits = pl.mode == kBits ? 2 : pl.bits;
+  // nw_align_bits as rolling strips (kBitsStrip): NWK_STRIP / opts.kernel 5
+  // force them (1) or band tasks (0); by default use_strips decides
+  int strip_ring = 0;
+  if (pl.mode == kBits) {
+    static const int strip_env = getenv("NWK_STRIP") ? atoi(getenv("NWK_STRIP")) : -1;
+    const int want = c->opts.kernel == 5 ? 1 : c->opts.kernel == 4 ? 0 : strip_env;
+    if (want != 0 && use_strips(c, work, sc.pgap, want == 1, &strip_ring)) pl.mode = kBitsStrip;
+  }
+  const bool bitsy = pl.mode == kBits || pl.mode == kBitsStrip;
+  st.bits = bitsy ? 2 : pl.bits;
   st.mode = pl.mode;
   int rc;
   HIP_TRY(hipSetDevice(c->device));
@@ -924,7 +1041,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   }
   if (!dp.empty()) {
     if ((rc = build_encoding(c, pl.kind)) != NWK_OK) return rc;
-    if (pl.mode == kBits && (rc = build_yw(c)) != NWK_OK) return rc;
+    if (bitsy && (rc = build_yw(c)) != NWK_OK) return rc;
     if ((pl.mode == kPacked || band_pairs(pl.mode)) &&
         (rc = build_sel(c, pl.K0 < 0 ? 1 : 0, band_pairs(pl.mode) ? 64 : 1)) != NWK_OK)
       return rc;
@@ -946,7 +1063,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   // more batches (C5: 4 of ~124 pairs, ~12 rounds of wave slots each).
   static const int win_env = getenv("NWK_BITS_WIN") ? atoi(getenv("NWK_BITS_WIN")) : -1;
   static const int winb_env = getenv("NWK_WIN_BATCHES") ? atoi(getenv("NWK_WIN_BATCHES")) : 0;
-  if ((pl.mode == kBits || pl.mode == kAffinePk) && !dp.empty() && win_env != 0) {
+  if ((bitsy || pl.mode == kAffinePk) && !dp.empty() && win_env != 0) {
     auto total_b = [&]() {
       int64_t mat = 0, bnd = 0, ops = 0;
       for (const auto& w : dp) mat += w.mat_dw, bnd += w.bnd_gr, ops += w.ops_b;
@@ -1002,7 +1119,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       acc += (double)w.m * w.n;
     }
   }
-  int bpc = pl.mode == kBits ? bits_blocks_per_cu(sc.pgap) : fill_blocks_per_cu(pl.mode, pl.bits);
+  int bpc = pl.mode == kBits        ? bits_blocks_per_cu(sc.pgap)
+            : pl.mode == kBitsStrip ? strip_blocks_per_cu(sc.pgap, strip_ring)
+                                    : fill_blocks_per_cu(pl.mode, pl.bits);
   // waves per SIMD: nw_align_pk2 measured best at 2 (band chains run at the
   // pace of their slowest member; more waves per SIMD only add waiting);
   // NWK_BPC overrides (experiments)
@@ -1012,7 +1131,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   if (pl.mode == kAffine) bpc = std::min(bpc, 2);
   if (pl.mode == kAffinePk) bpc = std::min(bpc, 2);
   static const int bpc_cap = getenv("NWK_BPC") ? atoi(getenv("NWK_BPC")) : 0;
-  if (bpc_cap > 0) bpc = std::min(bpc_cap, fill_blocks_per_cu(pl.mode, pl.bits));
+  if (bpc_cap > 0) bpc = std::min(bpc_cap, bitsy ? bpc : fill_blocks_per_cu(pl.mode, pl.bits));
   const int grid = bpc * c->cus;
   float ms = 0;
 
@@ -1130,15 +1249,20 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       PairDesc& d = pd[q];
       d.x_off = c->c_off[w.i];
       d.y_off = c->c_off[w.j];
-      d.e_off = pl.mode == kBits ? c->yw_off[w.j] : c->e_off[w.j];
+      d.e_off = bitsy ? c->yw_off[w.j] : c->e_off[w.j];
+      d.xw_off = pl.mode == kBitsStrip ? c->yw_off[w.i] : 0;
+      d.bits_np = pl.mode == kBitsStrip ? strip_np(w.n) : 0;
+      d.pad_ = 0;
       d.mat_off = mat_base_b / 4 + mo;
       d.bnd_off = bo;
       d.ops_off = ops_base_b + oo;
       d.m = w.m;
       d.n = w.n;
-      d.nbands = (int)ceil_div(w.m, pl.mode == kBits ? kBitsRows : kBandRows);
-      d.nchunks = (int)ceil_div(w.n, 64);
-      d.sblocks = pl.mode == kBits ? bits_sblocks(d.nchunks) : sblocks_of(pl.mode, d.nchunks);
+      d.nbands = (int)ceil_div(w.m, bitsy ? kBitsRows : kBandRows);
+      d.nchunks = pl.mode == kBitsStrip ? d.bits_np / 64 : (int)ceil_div(w.n, 64);
+      d.sblocks = pl.mode == kBits        ? bits_sblocks(d.nchunks)
+                  : pl.mode == kBitsStrip ? strip_sblocks(w.m, w.n)
+                                          : sblocks_of(pl.mode, d.nchunks);
       d.bits_w = w.bits_w;
       d.bits_nblk = w.bits_nblk;
       d.slot = q;
@@ -1172,6 +1296,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     static const int order_env = getenv("NWK_ORDER") ? atoi(getenv("NWK_ORDER")) : -1;
     int order = order_env;
     if (order < 0) order = (pl.mode == kBits || pl.mode == kAffinePk) && ntasks > 4 * (int64_t)grid ? 1 : 0;
+    if (pl.mode == kBitsStrip) order = 0;  // one task per pair, largest first
     if (order == 1) {  // band-major (experiment)
       for (int b = 0; b < maxb; ++b)
         for (int q = 0; q < np; ++q)
@@ -1240,7 +1365,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.dbg_notrace = (getenv("NWK_AFF_NOTRACE") || getenv("NWK_NOTRACE")) ? 1 : 0;
     fa.lin_mode = 0;
     fa.prog = nullptr;
-    fa.yw = pl.mode == kBits ? c->d_yw.as<unsigned>() : nullptr;
+    fa.yw = bitsy ? c->d_yw.as<unsigned>() : nullptr;
+    fa.strip_ring = strip_ring;
     fa.retry = c->d_retry.as<int>();
     if (getenv("NWK_WATCHDOG")) {
       if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;
@@ -1281,6 +1407,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     if (pl.mode == kBits)
       HIP_TRY(launch_bits(fa, sc.pxy, sc.pgap, (int)std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
+    else if (pl.mode == kBitsStrip)
+      HIP_TRY(launch_strip(fa, sc.pxy, sc.pgap, (int)std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     else
       HIP_TRY(launch_fill(pl.mode, pl.bits, fa, std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
@@ -1566,6 +1694,37 @@ int nwk_align_pairs(nwk_ctx* c, const int64_t* pair_ids, int64_t npairs, int32_t
   return align_pairs_sc(c, pair_ids, npairs, Scoring{pxy, pgap, false, 0, 0}, penalties, problem_hash);
 }
 
+int nwk_align_pairs_begin(nwk_ctx* c, const int64_t* pair_ids, int64_t npairs, int32_t pxy, int32_t pgap) {
+  if (!c || npairs < 0 || (npairs > 0 && !pair_ids)) return fail(NWK_EINVAL, "nwk_align_pairs_begin: bad argument");
+  if (c->pending) return fail(NWK_EINVAL, "nwk_align_pairs_begin: a call is already in flight on this context");
+  c->a_ids.assign(pair_ids, pair_ids + npairs);
+  c->a_pen.assign((size_t)std::max<int64_t>(npairs, 1), 0);
+  c->a_hash.assign((size_t)std::max<int64_t>(npairs, 1) * 64, 0);
+  c->pending = true;
+  c->a_rc = NWK_OK;
+  c->a_err.clear();
+  c->async = std::thread([c, pxy, pgap]() {
+    c->a_rc = nwk_align_pairs(c, c->a_ids.data(), (int64_t)c->a_ids.size(), pxy, pgap, c->a_pen.data(),
+                              c->a_hash.data());
+    if (c->a_rc != NWK_OK) c->a_err = g_err;
+  });
+  return NWK_OK;
+}
+
+int nwk_align_pairs_end(nwk_ctx* c, int32_t* penalties, uint8_t* problem_hash) {
+  if (!c || !c->pending) return fail(NWK_EINVAL, "nwk_align_pairs_end: no call in flight");
+  c->async.join();
+  c->pending = false;
+  if (c->a_rc != NWK_OK) return fail(c->a_rc, "%s", c->a_err.c_str());
+  const size_t n = c->a_ids.size();
+  if (n && (!penalties || !problem_hash)) return fail(NWK_EINVAL, "nwk_align_pairs_end: bad argument");
+  if (n) {
+    memcpy(penalties, c->a_pen.data(), 4 * n);
+    memcpy(problem_hash, c->a_hash.data(), 64 * n);
+  }
+  return NWK_OK;
+}
+
 int nwk_align_pairs_affine(nwk_ctx* c, const int64_t* pair_ids, int64_t npairs, int32_t pxy, int32_t go,
                            int32_t ge, int32_t* penalties, uint8_t* problem_hash) {
   return align_pairs_sc(c, pair_ids, npairs, Scoring{pxy, 0, true, go, ge}, penalties, problem_hash);
@@ -1591,8 +1750,7 @@ static int align_all_sc(nwk_ctx* c, const Scoring& sc, int32_t* penalties, uint8
   if ((rc = align_work(c, w, sc, penalties, problem_hash, nullptr, nullptr, &ch)) != NWK_OK) return rc;
   ch.advance();  // pairs with no DP cells, if they are the tail
   if (ch.next != P) return fail(NWK_EKERNEL, "nwk_align_all: chain stopped at pair %lld of %lld", (long long)ch.next, (long long)P);
-  memcpy(hash_hex, ch.buf, ch.la);
-  hash_hex[ch.la] = 0;
+  ch.hex(hash_hex);
   return NWK_OK;
 }
 
@@ -1706,18 +1864,111 @@ int nwk_finalize_moves(const uint8_t* x, int32_t m, const uint8_t* y, int32_t n,
 
 int nwk_chain_hash(const uint8_t* ph, int64_t P, char* hash_hex) {
   if (!hash_hex || (P > 0 && !ph)) return fail(NWK_EINVAL, "nwk_chain_hash: bad argument");
-  char buf[256];
-  size_t la = 0;  // acc starts as "" (skel:121)
-  for (int64_t p = 0; p < P; ++p) {
-    to_hex(ph + 64 * p, buf + la);
-    char acc[128];
-    sha512_hex(buf, la + 128, acc);
-    memcpy(buf, acc, 128);
-    la = 128;
-  }
-  memcpy(hash_hex, buf, la);
-  hash_hex[la] = 0;
+  Chain ch;
+  ch.hashes = ph;
+  ch.ready.assign((size_t)std::max<int64_t>(P, 0), 1);
+  ch.advance();
+  ch.hex(hash_hex);
   return NWK_OK;
+}
+
+// Streaming chain (skel:159 as results arrive, sub:305-337's collect-then-chain
+// overlapped): feed() stores records and computes their second-block schedules
+// on the caller's thread; a worker thread advances the chain over the ready
+// prefix of canonical ids while the caller goes on (e.g. aligning the next
+// chunk of its shard).
+}  // extern "C"
+
+struct nwk_chain {
+  int64_t P = 0;
+  std::vector<uint8_t> ph;       // [P][64]
+  std::vector<uint64_t> kw;      // [P][80] second-block schedules
+  std::vector<int32_t> pen;      // [P]
+  std::unique_ptr<std::atomic<char>[]> ready;
+  std::atomic<int64_t> fed{0};
+  int64_t next = 0;              // worker-owned
+  ChainAcc acc;
+  std::mutex mu;
+  std::condition_variable cv;
+  bool closed = false;
+  std::thread worker;
+  void run() {
+    for (;;) {
+      while (next < P && ready[next].load(std::memory_order_acquire)) {
+        chain_step(&acc, kw.data() + 80 * next);
+        ++next;
+      }
+      std::unique_lock<std::mutex> lk(mu);
+      if (next >= P) return;
+      if (ready[next].load(std::memory_order_acquire)) continue;
+      if (closed) return;
+      cv.wait(lk);
+    }
+  }
+};
+
+extern "C" {
+
+int nwk_chain_create(int64_t P, nwk_chain** out) {
+  if (!out || P < 0) return fail(NWK_EINVAL, "nwk_chain_create: bad argument");
+  std::unique_ptr<nwk_chain> ch(new nwk_chain);
+  ch->P = P;
+  ch->ph.assign((size_t)P * 64, 0);
+  ch->kw.assign((size_t)P * 80, 0);
+  ch->pen.assign((size_t)P, 0);
+  ch->ready.reset(new std::atomic<char>[(size_t)std::max<int64_t>(P, 1)]);
+  for (int64_t p = 0; p < P; ++p) ch->ready[p].store(0, std::memory_order_relaxed);
+  nwk_chain* c = ch.get();
+  ch->worker = std::thread([c]() { c->run(); });
+  *out = ch.release();
+  return NWK_OK;
+}
+
+int nwk_chain_feed(nwk_chain* ch, const int64_t* ids, const int32_t* penalties, const uint8_t* problem_hash,
+                   int64_t n) {
+  if (!ch || n < 0 || (n > 0 && (!ids || !problem_hash))) return fail(NWK_EINVAL, "nwk_chain_feed: bad argument");
+  for (int64_t q = 0; q < n; ++q)
+    if (ids[q] < 0 || ids[q] >= ch->P || ch->ready[ids[q]].load(std::memory_order_relaxed))
+      return fail(NWK_EINVAL, "nwk_chain_feed: pair id %lld out of range or fed twice", (long long)ids[q]);
+  for (int64_t q = 0; q < n; ++q) {
+    const int64_t p = ids[q];
+    memcpy(ch->ph.data() + 64 * p, problem_hash + 64 * q, 64);
+    if (penalties) ch->pen[p] = penalties[q];
+    chain_schedule(problem_hash + 64 * q, ch->kw.data() + 80 * p);
+    ch->ready[p].store(1, std::memory_order_release);
+  }
+  ch->fed += n;
+  { std::lock_guard<std::mutex> lk(ch->mu); }
+  ch->cv.notify_one();
+  return NWK_OK;
+}
+
+int nwk_chain_finish(nwk_chain* ch, char* hash_hex, int32_t* penalties, uint8_t* problem_hash) {
+  if (!ch || !hash_hex) return fail(NWK_EINVAL, "nwk_chain_finish: bad argument");
+  {
+    std::lock_guard<std::mutex> lk(ch->mu);
+    ch->closed = true;
+  }
+  ch->cv.notify_one();
+  if (ch->worker.joinable()) ch->worker.join();
+  if (ch->next != ch->P)
+    return fail(NWK_EINVAL, "nwk_chain_finish: pair %lld of %lld was never fed", (long long)ch->next, (long long)ch->P);
+  chain_hex(ch->acc, hash_hex);
+  hash_hex[ch->acc.empty ? 0 : 128] = 0;
+  if (penalties && ch->P) memcpy(penalties, ch->pen.data(), 4 * (size_t)ch->P);
+  if (problem_hash && ch->P) memcpy(problem_hash, ch->ph.data(), 64 * (size_t)ch->P);
+  return NWK_OK;
+}
+
+void nwk_chain_destroy(nwk_chain* ch) {
+  if (!ch) return;
+  {
+    std::lock_guard<std::mutex> lk(ch->mu);
+    ch->closed = true;
+  }
+  ch->cv.notify_one();
+  if (ch->worker.joinable()) ch->worker.join();
+  delete ch;
 }
 
 void nwk_sha512_hex(const uint8_t* data, int64_t len, char* out_hex) {

@@ -77,13 +77,122 @@ void compress(uint64_t st[8], const unsigned char* blk) {
   st[0] += a; st[1] += b; st[2] += c; st[3] += d;
   st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
+// Compression over a precomputed K + W schedule (the chain's fixed blocks).
+void compress_kw(uint64_t st[8], const uint64_t kw[80]) {
+  uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#define NWK_RKW(a, b, c, d, e, f, g, h, t)                                      \
+  do {                                                                        \
+    const uint64_t t1 = h + NWK_S1(e) + (g ^ (e & (f ^ g))) + kw[t];           \
+    const uint64_t t2 = NWK_S0(a) + ((a & b) | (c & (a | b)));                \
+    d += t1;                                                                  \
+    h = t1 + t2;                                                              \
+  } while (0)
+#pragma unroll
+  for (int t = 0; t < 80; t += 8) {
+    NWK_RKW(a, b, c, d, e, f, g, h, t + 0);
+    NWK_RKW(h, a, b, c, d, e, f, g, t + 1);
+    NWK_RKW(g, h, a, b, c, d, e, f, t + 2);
+    NWK_RKW(f, g, h, a, b, c, d, e, t + 3);
+    NWK_RKW(e, f, g, h, a, b, c, d, t + 4);
+    NWK_RKW(d, e, f, g, h, a, b, c, t + 5);
+    NWK_RKW(c, d, e, f, g, h, a, b, t + 6);
+    NWK_RKW(b, c, d, e, f, g, h, a, t + 7);
+  }
+#undef NWK_RKW
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+  st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// K + W of a block given as 16 big-endian words
+void schedule_kw(const uint64_t w16[16], uint64_t kw[80]) {
+  uint64_t w[80];
+  for (int t = 0; t < 16; ++t) w[t] = w16[t];
+  for (int t = 16; t < 80; ++t) w[t] = NWK_s1(w[t - 2]) + w[t - 7] + NWK_s0(w[t - 15]) + w[t - 16];
+  for (int t = 0; t < 80; ++t) kw[t] = kK[t] + w[t];
+}
+
 #undef NWK_ROUND
 #undef NWK_S0
 #undef NWK_S1
 #undef NWK_s0
 #undef NWK_s1
 
+// The 8 lowercase hex digits of the low 32 bits of x, most significant first,
+// as one big-endian message word (SWAR: nibbles spread to bytes, +'0', +39
+// more for a..f).
+inline uint64_t hex_word(uint64_t x) {
+  x &= 0xffffffffULL;
+  x = (x | (x << 16)) & 0x0000FFFF0000FFFFULL;
+  x = (x | (x << 8)) & 0x00FF00FF00FF00FFULL;
+  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0FULL;
+  const uint64_t gt9 = ((x + 0x0606060606060606ULL) >> 4) & 0x0101010101010101ULL;
+  return x + 0x3030303030303030ULL + gt9 * 0x27;
+}
+
+// the hex block of a 64-byte digest given as 8 big-endian words
+inline void hex_block(const uint64_t d[8], uint64_t w16[16]) {
+  for (int q = 0; q < 8; ++q) {
+    w16[2 * q] = hex_word(d[q] >> 32);
+    w16[2 * q + 1] = hex_word(d[q]);
+  }
+}
+
+const uint64_t kIV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                         0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                         0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+
+// padding blocks of 128- and 256-byte messages: 0x80, zeros, the bit length
+struct PadKW {
+  uint64_t kw128[80], kw256[80];
+  PadKW() {
+    uint64_t w[16] = {0x8000000000000000ULL};
+    w[15] = 128 * 8;
+    schedule_kw(w, kw128);
+    w[15] = 256 * 8;
+    schedule_kw(w, kw256);
+  }
+};
+const PadKW& pad_kw() {
+  static const PadKW p;
+  return p;
+}
+
 }  // namespace
+
+void chain_schedule(const unsigned char ph[64], uint64_t kw[80]) {
+  uint64_t d[8], w16[16];
+  for (int q = 0; q < 8; ++q) d[q] = load_be64(ph + 8 * q);
+  hex_block(d, w16);
+  schedule_kw(w16, kw);
+}
+
+void chain_step(ChainAcc* acc, const uint64_t kw[80]) {
+  uint64_t st[8];
+  memcpy(st, kIV, sizeof st);
+  if (acc->empty) {  // message = hex(ph): its block, then the padding of a 128-byte message
+    compress_kw(st, kw);
+    compress_kw(st, pad_kw().kw128);
+    acc->empty = false;
+  } else {           // message = hex(acc) ++ hex(ph), then the padding of a 256-byte message
+    uint64_t w16[16], kw1[80];
+    hex_block(acc->dig, w16);
+    schedule_kw(w16, kw1);
+    compress_kw(st, kw1);
+    compress_kw(st, kw);
+    compress_kw(st, pad_kw().kw256);
+  }
+  memcpy(acc->dig, st, sizeof st);
+}
+
+void chain_hex(const ChainAcc& acc, char hex[128]) {
+  if (acc.empty) return;
+  unsigned char raw[64];
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t v = __builtin_bswap64(acc.dig[i]);
+    memcpy(raw + 8 * i, &v, 8);
+  }
+  to_hex(raw, hex);
+}
 
 void Sha512::reset() {
   static const uint64_t iv[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,

@@ -85,6 +85,100 @@ def all_gather_records(rec, device=None, group=None):
     return out.cpu().numpy()
 
 
+def unpack_chunk(gathered):
+    """(ids, penalties, hashes) of the valid records of one chunk's all-gather.
+    Raises RankFailed on every rank when some rank contributed FAILED records."""
+    g = np.ascontiguousarray(gathered, dtype=np.uint8).reshape(-1, REC)
+    head = g[:, :8].copy().view(np.int32).reshape(-1, 2)
+    if (head[:, 0] == FAILED).any():
+        raise RankFailed("all-gather: a rank failed to align its shard")
+    ok = head[:, 0] >= 0
+    return head[ok, 0].astype(np.int64), head[ok, 1].copy(), g[ok, 8:]
+
+
+def chunk_parts(lengths, rank, world, chunks):
+    """This rank's shard cut at global canonical thresholds P*c/chunks, and for
+    every chunk the largest part over ranks (the padded record block size)."""
+    k = len(lengths)
+    P = k * (k - 1) // 2
+    bounds = [P * c // chunks for c in range(chunks + 1)]
+    cut = lambda ids, c: ids[(ids >= bounds[c]) & (ids < bounds[c + 1])]
+    shards = [seqalign.shard_pairs(lengths, r, world) for r in range(world)]
+    per = [max([len(cut(sh, c)) for sh in shards] + [1]) for c in range(chunks)]
+    return [cut(shards[rank], c) for c in range(chunks)], per
+
+
+def auto_chunks(P, world):
+    """Pieces per rank: the chain of skel:159 costs ~0.25 us per link on the
+    host, so jobs of many pairs (C4: 32,640) hide all but the last piece's
+    links behind the alignment; small jobs keep one piece (one launch)."""
+    return 2 if P >= 8192 and world > 1 else 1
+
+
+def align_sharded_pipelined(eng, lengths, pxy, pgap, rank, world, chunks=1, device=None, group=None,
+                            on_piece=None):
+    """The shard in `chunks` pieces of ascending canonical ids: piece c+1 aligns
+    on the GPU (Engine.align_pairs_begin) while piece c's records go through
+    their all-gather and rank 0's chain worker (seqalign.ChainStream) advances
+    over them -- sub:305-337 collects results as they arrive and then chains;
+    here the chain of all but the last piece hides behind the alignment.
+    Returns (hash on rank 0 else None, penalties[P], hashes[P,64]) on rank 0,
+    (None, None, None) elsewhere.  Same failure contract as align_sharded:
+    a failing rank joins every remaining collective with FAILED records."""
+    k = len(lengths)
+    P = k * (k - 1) // 2
+    parts, per = chunk_parts(lengths, rank, world, chunks)
+    chain = seqalign.ChainStream(P) if rank == 0 else None
+    err = None       # this rank's failure, or a peer's seen in a gather
+    pending = False  # an align_pairs_begin not yet ended
+    try:
+        try:
+            eng.align_pairs_begin(parts[0], pxy, pgap)
+            pending = True
+        except Exception as e:
+            err = e
+        for c in range(chunks):
+            rec = None
+            if err is None:
+                try:
+                    pending = False
+                    pen, hs = eng.align_pairs_end()
+                    if on_piece is not None:
+                        on_piece(c)
+                    if c + 1 < chunks:
+                        eng.align_pairs_begin(parts[c + 1], pxy, pgap)
+                        pending = True
+                    rec = pack_records(parts[c], pen, hs, per[c])
+                except Exception as e:
+                    err = e
+            if rec is None:  # still join the collective, so no peer waits forever
+                rec = pack_records([], [], [], per[c])
+                rec[:, :4] = np.array([FAILED], dtype=np.int32).view(np.uint8)
+            g = all_gather_records(rec, device=device, group=group)
+            if err is not None:
+                continue
+            try:
+                ids, pen, hs = unpack_chunk(g)
+            except RankFailed as e:  # every rank sees it in the same gather
+                err = e
+                continue
+            if chain is not None:
+                chain.feed(ids, pen, hs)
+        if err is not None:
+            raise RankFailed("rank %d: %s" % (rank, err)) from err
+        if chain is None:
+            return None, None, None
+        return chain.finish()
+    finally:
+        if pending:  # a peer failed while this rank's next piece was in flight
+            try:
+                eng.align_pairs_end()
+            except Exception:
+                pass
+        if chain is not None:
+            chain.close()
+
+
 def align_sharded(align_fn, lengths, pxy, pgap, rank, world, device=None, group=None):
     """Runs this rank's shard through align_fn(ids, pxy, pgap) -> (pen, hashes),
     gathers every rank's records and returns (penalties[P], hashes[P,64], ids)."""

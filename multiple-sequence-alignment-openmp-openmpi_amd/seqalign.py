@@ -24,10 +24,10 @@ LIB_PATH = os.path.join(HERE, "lib", "libnwk.so")
 NWK_OK = 0
 ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "EKERNEL", -5: "ECOMM"}
 MODES = {0: "profile", 1: "compare", 2: "literal", 3: "affine", 4: "packed-profile", 5: "packed-band-pairs",
-         7: "packed-affine-band-pairs", 8: "bit-sliced-planes"}
+         7: "packed-affine-band-pairs", 8: "bit-sliced-planes", 9: "bit-sliced-strips"}
 # fill kernel of each mode (csrc/nwk_kernels.hip), as rocprofv3 names it
 KERNELS = {0: "nw_align", 1: "nw_align", 2: "nw_align", 3: "nw_align_affine", 4: "nw_align_pk", 5: "nw_align_pk2",
-           7: "nw_align_pka", 8: "nw_align_bits"}
+           7: "nw_align_pka", 8: "nw_align_bits", 9: "nw_align_strip"}
 
 
 class NwkError(RuntimeError):
@@ -78,6 +78,12 @@ SIGNATURES = {
     "nwk_chain_hash": (ctypes.c_int, [_P, _I64, _P]),
     "nwk_finalize_moves": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P]),
     "nwk_sha512_hex": (None, [_P, _I64, _P]),
+    "nwk_align_pairs_begin": (ctypes.c_int, [_P, _P, _I64, _I32, _I32]),
+    "nwk_align_pairs_end": (ctypes.c_int, [_P, _P, _P]),
+    "nwk_chain_create": (ctypes.c_int, [_I64, _P]),
+    "nwk_chain_feed": (ctypes.c_int, [_P, _P, _P, _P, _I64]),
+    "nwk_chain_finish": (ctypes.c_int, [_P, _P, _P, _P]),
+    "nwk_chain_destroy": (None, [_P]),
 }
 
 _lib = None
@@ -88,6 +94,7 @@ _lib = None
 # kernel build that produced them.
 KERNEL_SOURCES = {
     "nw_align_bits": ("csrc/nwk_bits.hip", "csrc/nwk_internal.h", "Makefile"),
+    "nw_align_strip": ("csrc/nwk_bits.hip", "csrc/nwk_internal.h", "Makefile"),
     "nw_align_pka": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
     "nw_align_pk2": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
     "nw_align_pk": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
@@ -173,7 +180,7 @@ class Engine:
 
     FINALIZE = {"auto": 0, "host": 1, "device": 2}
 
-    KERNEL = {"auto": 0, "nw_align": 1, "nw_align_pk": 2, "nw_align_pk2": 3, "nw_align_bits": 4}
+    KERNEL = {"auto": 0, "nw_align": 1, "nw_align_pk": 2, "nw_align_pk2": 3, "nw_align_bits": 4, "nw_align_strip": 5}
 
     def __init__(self, device=0, bits=0, workspace_bytes=0, host_threads=0, verbose=False, finalize="auto",
                  linear_space=0, kernel="auto"):
@@ -194,6 +201,7 @@ class Engine:
         _check(self.lib.nwk_ctx_create(ctypes.byref(o), ctypes.byref(self._ctx)))
         self.k = 0
         self._offs = None
+        self._pending = 0
 
     def close(self):
         if self._ctx:
@@ -225,6 +233,20 @@ class Engine:
         pen = np.zeros(max(n, 1), dtype=np.int32)
         hs = np.zeros((max(n, 1), 64), dtype=np.uint8)
         _check(self.lib.nwk_align_pairs(self._ctx, _ptr(ids), n, pxy, pgap, _ptr(pen), _ptr(hs)))
+        return pen[:n], hs[:n]
+
+    def align_pairs_begin(self, pair_ids, pxy, pgap):
+        """Starts align_pairs on the context's host thread and returns at once
+        (nwk_align_pairs_begin); align_pairs_end() collects the result."""
+        ids = np.ascontiguousarray(pair_ids, dtype=np.int64)
+        _check(self.lib.nwk_align_pairs_begin(self._ctx, _ptr(ids), ids.size, pxy, pgap))
+        self._pending = ids.size
+
+    def align_pairs_end(self):
+        n = self._pending
+        pen = np.zeros(max(n, 1), dtype=np.int32)
+        hs = np.zeros((max(n, 1), 64), dtype=np.uint8)
+        _check(self.lib.nwk_align_pairs_end(self._ctx, _ptr(pen), _ptr(hs)))
         return pen[:n], hs[:n]
 
     def align_all(self, pxy, pgap, affine=None):
@@ -290,6 +312,43 @@ class Engine:
         _check(self.lib.nwk_msa(self._ctx, pxy, pgap, _ptr(pen) if pen.size else None, _ptr(rows), cap,
                                 ctypes.byref(ln), ctypes.byref(sop)))
         return [bytes(rows[r, :ln.value]) for r in range(self.k)], sop.value
+
+
+class ChainStream:
+    """nwk_chain_*: the skel:159 chain over P pairs, advanced by a C++ worker
+    thread as records are fed in any order; finish() -> (hash, penalties[P],
+    hashes[P, 64]) in canonical order."""
+
+    def __init__(self, P):
+        self.lib = load_library()
+        self.P = P
+        self._ch = ctypes.c_void_p()
+        _check(self.lib.nwk_chain_create(P, ctypes.byref(self._ch)))
+
+    def feed(self, ids, penalties, hashes):
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        pen = np.ascontiguousarray(penalties, dtype=np.int32)
+        hs = np.ascontiguousarray(hashes, dtype=np.uint8).reshape(-1, 64)
+        if ids.size:
+            _check(self.lib.nwk_chain_feed(self._ch, _ptr(ids), _ptr(pen), _ptr(hs), ids.size))
+
+    def finish(self):
+        out = ctypes.create_string_buffer(129)
+        pen = np.zeros(max(self.P, 1), dtype=np.int32)
+        hs = np.zeros((max(self.P, 1), 64), dtype=np.uint8)
+        _check(self.lib.nwk_chain_finish(self._ch, out, _ptr(pen), _ptr(hs)))
+        return out.value.decode(), pen[:self.P], hs[:self.P]
+
+    def close(self):
+        if self._ch:
+            self.lib.nwk_chain_destroy(self._ch)
+            self._ch = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def chain_hash(problem_hashes):

@@ -131,3 +131,108 @@ def test_gloo_failing_rank_raises_everywhere(world):
     for r, msg in out.items():
         assert msg.startswith("raised:"), (r, msg)
     assert "injected" in out[1]
+
+
+class _OracleEngine:
+    """Test stand-in for seqalign.Engine's begin/end pair (the CPU oracle as
+    the per-rank aligner -- test infrastructure; there is no GPU here).
+    fail_at: raise in the end() of that piece."""
+
+    def __init__(self, genes, fail_at=None):
+        self.genes, self.fail_at, self.calls, self.ids = genes, fail_at, 0, None
+
+    def align_pairs_begin(self, ids, pxy, pgap):
+        assert self.ids is None, "one piece in flight"
+        self.ids, self.pxy, self.pgap = list(ids), pxy, pgap
+
+    def align_pairs_end(self):
+        import numpy as np
+
+        import oracle
+        import seqalign
+
+        ids, self.ids = self.ids, None
+        self.calls += 1
+        if self.fail_at is not None and self.calls - 1 == self.fail_at:
+            raise RuntimeError("injected NWK_EKERNEL in piece %d" % self.fail_at)
+        pen, hs = [], []
+        for p in ids:
+            i, j = seqalign.pair_ij(int(p))
+            pe, a1, a2 = oracle.pair(self.genes[i], self.genes[j], self.pxy, self.pgap)
+            pen.append(pe)
+            hs.append(list(bytes.fromhex(oracle.problem_hash(a1, a2))))
+        return np.array(pen, dtype=np.int32), np.array(hs, dtype=np.uint8).reshape(-1, 64)
+
+
+def _pipelined_worker(rank, world, port, cases, chunks, fail, q):
+    import sys
+
+    for p in (PKG, ORACLE):
+        sys.path.insert(0, p)
+    import dist as nwdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        for name, pxy, pgap, genes in cases:
+            eng = _OracleEngine(genes, fail_at=1 if (fail and rank == 1) else None)
+            try:
+                h, pen, _ = nwdist.align_sharded_pipelined(eng, [len(g) for g in genes], pxy, pgap, rank, world,
+                                                           chunks=chunks)
+                q.put((rank, name, h, None if pen is None else [int(v) for v in pen]))
+            except nwdist.RankFailed as e:
+                q.put((rank, name, "raised: %s" % e, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 1), (2, 3), (3, 2), (3, 5)])
+def test_gloo_pipelined_chunks_match_golden(world, chunks):
+    """dist.align_sharded_pipelined: each rank's shard in pieces of ascending
+    canonical ids, one all-gather per piece while the next piece aligns, rank
+    0's streaming chain (nwk_chain_*) fed per piece -- the answer hash and
+    penalties of the reference (golden) for any number of pieces."""
+    cases = []
+    for c in CASES:
+        pxy, pgap, genes = case_input(c)
+        cases.append((c["name"], pxy, pgap, genes))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, cases, chunks, False, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world * len(cases))]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    gold = {c["name"]: c for c in CASES}
+    for rank, name, h, pen in out:
+        if rank == 0:
+            assert h == gold[name]["hash"], name
+            assert pen == gold[name]["penalties"], name
+        else:
+            assert h is None
+
+
+def test_gloo_pipelined_failing_piece_raises_everywhere():
+    """Rank 1's second piece fails while its third is pending: it joins every
+    remaining all-gather with FAILED records and all ranks raise (none hangs)."""
+    genes = [b"ACGT" * 5, b"AC" * 7, b"GATTACA", b"T" * 11, b"CAT" * 4, b"GG" * 6, b"TACG" * 3]
+    cases = [("f", 3, 2, genes)]
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, cases, 4, True, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {r: h for r, _, h, _ in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r, msg in out.items():
+        assert isinstance(msg, str) and msg.startswith("raised:"), (r, msg)
+    assert "injected" in out[1]

@@ -120,6 +120,60 @@ def test_bits_kernel_every_mismatch_level(pxy, pgap):
     assert [x.tobytes().hex() for x in hs] == ohs
 
 
+def _strip_pairs(ncols, k):
+    """Canonical ids of the pairs whose column sequence is one of the first
+    ncols genes (strips need n in range; rows can be anything)."""
+    return np.array([seqalign.pair_index(i, j) for i in range(1, k) for j in range(min(i, ncols))],
+                    dtype=np.int64)
+
+
+@pytest.mark.parametrize("pxy,pgap", BITS_PENALTIES)
+def test_strip_kernel_every_mismatch_level(pxy, pgap):
+    """nw_align_strip (rolling strips: one wave sweeps every 2048-row pass of
+    a pair, csrc/nwk_bits.hip) at every mismatch level SR, forced
+    (kernel="nw_align_strip"): column lengths at the n' = n + 32 edge (4064 ->
+    4096) and just past the smallest admissible n' (4001), rows of one row, a
+    lane word, one pass exactly, one row past a pass, a ragged two-pass strip;
+    bit-exact against the oracle."""
+    r = random.Random(pxy * 37 + pgap)
+    genes = [bytes(r.choice(ACGT) for _ in range(L)) for L in (4001, 4064, 1, 33, 2048, 2049, 4100)]
+    ids = _strip_pairs(2, len(genes))
+    with seqalign.Engine(device=0, kernel="nw_align_strip") as e:
+        e.set_sequences(genes)
+        pen, hs = e.align_pairs(ids, pxy, pgap)
+        assert e.stats()["mode"] == 9, "nw_align_strip expected"
+    _, opens, ohs = oracle.all_pairs(genes, pxy, pgap)
+    assert [int(v) for v in pen] == [opens[i] for i in ids]
+    assert [x.tobytes().hex() for x in hs] == [ohs[i] for i in ids]
+
+
+@pytest.mark.parametrize("pxy,pgap", [(3, 2), (5, 1)])
+def test_strip_kernel_multi_pass_and_mutants(pxy, pgap):
+    """Strips over 1-5 row passes (rows up to 9000, a partial last pass),
+    columns 6000/8000 (C4's length), mutated copies (long diagonal runs, paths
+    off the diagonal) and swapped halves (a path ~2500 columns off it), under
+    the default workspace and under one small enough to force windowed storage
+    (with re-runs for paths that leave it); bit-exact against the oracle."""
+    r = random.Random(991 + pxy)
+    base = bytes(r.choice(ACGT) for _ in range(7000))
+    P, Q = (bytes(r.choice(ACGT) for _ in range(2500)) for _ in range(2))
+    cols = [bytes(r.choice(ACGT) for _ in range(L)) for L in (6000, 8000)] + _mutants(r, base, 1, ACGT) + [P + Q]
+    rows = [bytes(r.choice(ACGT) for _ in range(L)) for L in (2047, 6145, 9000)] + _mutants(r, base, 1, ACGT) + [Q + P]
+    genes = cols + rows
+    ids = _strip_pairs(len(cols), len(genes))
+    _, opens, ohs = oracle.all_pairs(genes, pxy, pgap)
+    for ws in (0, 40 << 20):
+        with seqalign.Engine(device=0, kernel="nw_align_strip", workspace_bytes=ws) as e:
+            e.set_sequences(genes)
+            pen, hs = e.align_pairs(ids, pxy, pgap)
+            st = e.stats()
+        assert st["mode"] == 9
+        if ws:
+            assert st["window"] > 0 or st["batches"] > 1, st
+        assert [int(v) for v in pen] == [opens[i] for i in ids], ws
+        assert [x.tobytes().hex() for x in hs] == [ohs[i] for i in ids], ws
+
+
 _ORDER_SCRIPT = r"""
 import json, sys
 import numpy as np

@@ -53,6 +53,42 @@ def test_chain_hash_matches_reference_stream(golden):
     assert seqalign.chain_hash(np.zeros((0, 64), dtype=np.uint8)) == ""
 
 
+@pytest.mark.parametrize("P", [0, 1, 2, 3, 300])
+def test_chain_stream_any_order_equals_chain(P):
+    """nwk_chain_* (the skel:159 chain advanced by a worker thread as records
+    arrive) fed in random chunks and order equals the one-shot chain, which
+    equals hashlib's sha512 over the concatenations (skel:155-159 contract)."""
+    rnd = np.random.RandomState(P)
+    hs = rnd.randint(0, 256, size=(P, 64)).astype(np.uint8)
+    pen = rnd.randint(0, 10 ** 6, size=P).astype(np.int32)
+    acc = ""
+    for p in range(P):
+        acc = hashlib.sha512((acc + hs[p].tobytes().hex()).encode()).hexdigest()
+    assert seqalign.chain_hash(hs) == acc
+    ch = seqalign.ChainStream(P)
+    order = rnd.permutation(P)
+    for part in np.array_split(order, min(P, 7) or 1):
+        ch.feed(part, pen[part], hs[part])
+    h, pen2, hs2 = ch.finish()
+    ch.close()
+    assert h == acc
+    assert (pen2 == pen).all() and (hs2 == hs).all()
+
+
+def test_chain_stream_rejects_missing_and_duplicate_pairs():
+    hs = np.zeros((4, 64), dtype=np.uint8)
+    ch = seqalign.ChainStream(4)
+    ch.feed([0, 2], [0, 0], hs[:2])
+    with pytest.raises(seqalign.NwkError):
+        ch.feed([2], [0], hs[:1])  # fed twice
+    with pytest.raises(seqalign.NwkError):
+        ch.feed([4], [0], hs[:1])  # out of range
+    with pytest.raises(seqalign.NwkError) as e:
+        ch.finish()  # pairs 1 and 3 never fed
+    assert "never fed" in str(e.value)
+    ch.close()
+
+
 def test_pair_index_roundtrip():
     p = 0
     for i in range(1, 300):
@@ -126,7 +162,7 @@ def test_no_device_fails_loudly(lib):
         seqalign.getMinimumPenalties([b"AC", b"CA"], 2, 3, 2, [0])
 
 
-@pytest.mark.parametrize("field,value", [("kernel", 5), ("kernel", -1), ("finalize", 3), ("bits", 5)])
+@pytest.mark.parametrize("field,value", [("kernel", 6), ("kernel", -1), ("finalize", 3), ("bits", 5)])
 def test_ctx_create_rejects_bad_options(lib, field, value):
     """nwk_ctx_create checks its options before looking for a device: a bad
     kernel / finalize / bits value is NWK_EINVAL with or without a GPU."""
