@@ -256,13 +256,13 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
 // for a full re-run when its path leaves.  With w >= 2048 rows' worth this
 // keeps nearly every word; at C4's w = 1024 about half of them, which halves
 // the HBM writes of the stored blocks.
-__device__ __forceinline__ bool bits_lane_stored(int64_t hi, int64_t lim, int64_t span) {
-  return hi >= -lim && hi - span <= lim;
+__device__ __forceinline__ bool bits_lane_stored(int64_t hi, int64_t lim, int64_t hlim) {
+  return hi >= -lim && hi <= hlim;  // hlim = w m + 38 m + 31 n: the span's low end <= w m
 }
 
 // Traceback of one pair from (m, n) over the stored (diag, up) bits.  A tile
 // is 64 steps (lane L holds step ts - L) of two row-lanes (tt and tt - 1),
-// four dwords per lane; the walk reads one bit word per move by v_readlane.
+// four dwords per lane; the walk goes by diagonal runs (see the loop).
 #define BITS_PROG(v)                                                                                         \
   do {                                                                                                       \
     if (prog && lane == 0) __hip_atomic_store((gu32*)prog, (unsigned)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
@@ -308,7 +308,8 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
   // cell (i = b 2048 + r), |dev| <= win m, else the path has left them
   int64_t dev = (int64_t)c * pd.m - (int64_t)(b * kBR + r) * pd.n;
   const int64_t lim = (int64_t)win * pd.m, dD = (int64_t)pd.n - pd.m;
-  if (win > 0 && c >= 0 && (dev > lim || dev < -lim)) out = true;
+  const bool lwin = bits_lane_window(win);
+  if (lwin && c >= 0 && (dev > lim || dev < -lim)) out = true;
   while (!out && c >= 0 && (b > 0 || r >= 0)) {
     if (r < 0) {  // into the band above
       --b;
@@ -343,43 +344,72 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
         }
       }
     }
-    // walk inside the tile
+    // Walk inside the tile by diagonal runs.  From the current cell (row r,
+    // lane L = ts - s) the path takes D moves while the diag bit is set: cell
+    // j of the run is row r - j at lane L + 2 j, so every lane tests the cell
+    // it holds, one ballot marks where the run stops and one find-first-set
+    // gives its length.  The stopping cell's U / L move is read with one
+    // v_readlane, and the run plus that move go to the LDS ring in one masked
+    // store.  Random pairs' paths are ~80% D moves, so one iteration covers
+    // ~6 moves where the move-by-move walk spent ~50 instructions per move.
+    const int rowlo = tt > 0 ? 32 * (tt - 1) : 0;  // lowest row of the tile
     for (;;) {
-      if (win > 0 && (dev > lim || dev < -lim)) {  // this cell is outside the stored lane words
+      if (lwin && (dev > lim || dev < -lim)) {  // this cell is outside the stored lane words
         out = true;
         break;
       }
-      // straight-line uniform code: one select per word, one v_readlane each
-      const int L = __builtin_amdgcn_readfirstlane(ts - s);
-      const bool hi = __builtin_amdgcn_readfirstlane(t - tt) == 0;
-      const unsigned vds = hi ? vd0 : vd1, vus = hi ? vu0 : vu1;
-      const unsigned d = (unsigned)__builtin_amdgcn_readlane((int)vds, L);
-      const unsigned u = (unsigned)__builtin_amdgcn_readlane((int)vus, L);
-      const int bit = r & 31;
-      unsigned op;
-      if ((d >> bit) & 1u) {
-        op = 'D';
-        --r;
-        --c;
-        s -= 2;
-        dev += dD;
-      } else if (!((u >> bit) & 1u)) {  // up: v == 0 (the stored word is v's plane 0)
-        op = 'U';
+      if (Lc - flushed >= 192) flush(Lc & ~3);  // (an iteration adds <= 33 bytes to the 256-byte ring)
+      const int L = ts - s;  // lane of the current step
+      // the run's cells j = 0 .. jmax are readable: in the tile's lanes and
+      // rows, columns >= 0, stored steps (>= slo)
+      int jmax = (63 - L) >> 1;
+      jmax = min(jmax, r - rowlo);
+      jmax = min(jmax, c);
+      jmax = min(jmax, (s - slo) >> 1);
+      const int off = lane - L, jl = off >> 1, row = r - jl;
+      bool stop = false;
+      if (off >= 0 && !(off & 1) && jl <= jmax) {
+        const unsigned w = (row >> 5) == tt ? vd0 : vd1;
+        stop = ((w >> (row & 31)) & 1u) == 0u;
+      }
+      const u64 stops = __builtin_amdgcn_ballot_w64(stop);
+      const int jn = stops ? (((int)__builtin_ctzll(stops) - L) >> 1) : jmax + 1;  // first non-D cell
+      if (lwin) {  // the run's cells (dev is linear along it: check its far end)
+        const int64_t de = dev + (int64_t)min(jn, jmax) * dD;
+        if (de > lim || de < -lim) {
+          out = true;
+          break;
+        }
+      }
+      const int nD = jn;  // D moves (cells 0 .. jn - 1)
+      unsigned op = 0;
+      if (jn <= jmax) {  // the run stops on a readable cell: its move is U (v == 0) or L
+        const int rr = r - jn;
+        const unsigned uw = (rr >> 5) == tt ? vu0 : vu1;
+        const unsigned u = (unsigned)__builtin_amdgcn_readlane((int)uw, L + 2 * jn);
+        op = ((u >> (rr & 31)) & 1u) ? 'L' : 'U';
+      }
+      const int nw = nD + (op ? 1 : 0);
+      if (lane < nw)
+        asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((Lc + lane) & 255)), "v"(lane < nD ? 'D' : op)
+                     : "memory");
+      Lc += nw;
+      r -= nD;
+      c -= nD;
+      s -= 2 * nD;
+      dev += (int64_t)nD * dD;
+      if (op == 'U') {
         --r;
         s -= 1;
         dev += pd.n;
-      } else {
-        op = 'L';
+      } else if (op == 'L') {
         --c;
         s -= 1;
         dev -= pd.m;
       }
-      asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(op) : "memory");
-      ++Lc;
-      if (Lc - flushed >= 192) flush(Lc & ~3);
       if (c < 0 || r < 0) break;
-      t = r >> 5;
-      if (s <= ts - 64 || (t != tt && t != tt - 1) || s < slo) break;
+      const int t2 = r >> 5;
+      if (s <= ts - 64 || (t2 != tt && t2 != tt - 1) || s < slo) break;
     }
     if (out) break;
     if (Lc > pd.m + pd.n) {
@@ -459,10 +489,11 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
     u64* gout = a.bnd + pd.bnd_off + (int64_t)band * nch * NG;
     const int nblk = pd.bits_nblk, blo = bits_blk_lo(band, pd.m, pd.n, pd.bits_w);
     unsigned* mb = a.mat + pd.mat_off + (int64_t)band * nblk * 1024 + lane * 4;
-    // windowed: per-lane store predicate (bits_lane_stored) for rows R0 + 32 lane ..
-    const bool lwin = pd.bits_w > 0;
-    const int64_t lim = (int64_t)pd.bits_w * pd.m, span = 38ll * pd.m + 31ll * pd.n;
-    const int64_t negRn = -(int64_t)(R0 + 32 * lane) * pd.n;
+    // windowed, w < 2048: per-lane store predicate (bits_lane_stored) for rows
+    // R0 + 32 lane ..; hi of the block at step s0 = hi0 + s0 m
+    const bool lwin = bits_lane_window(pd.bits_w);
+    const int64_t lim = (int64_t)pd.bits_w * pd.m, hlim = lim + 38ll * pd.m + 31ll * pd.n;
+    const int64_t hi0 = (int64_t)(7 - 32 * lane) * pd.m - (int64_t)(R0 + 32 * lane) * pd.n;
     // y windows: lane t's window for the half starting at step s_h is position s_h - 32 t
     const unsigned* ywp = a.yw + 2 * (pd.e_off - 32 * (int64_t)lane);
     unsigned yp0 = 0, yp1 = 0;
@@ -521,7 +552,8 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
         const bool sto = (unsigned)rel < (unsigned)nblk;
         unsigned* st = mb + (int64_t)rel * 1024;
         const int eh = s0 - 32 * lane;
-        const bool ls = !lwin || bits_lane_stored((int64_t)(eh + 7) * pd.m + negRn, lim, span);
+        bool ls = true;
+        if (lwin) ls = bits_lane_stored(hi0 + (int64_t)s0 * pd.m, lim, hlim);
         if (mask) {
           if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
           else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
@@ -658,8 +690,10 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
     const bool win = pd.bits_w > 0;
     const int nblk = pd.bits_nblk;
     int kw = 0, blo = win ? strip_blk_lo(0, pd.m, pd.n, np, pd.bits_w) : 0;  // current storage window
-    // per-lane store predicate (bits_lane_stored) for the rows of the lane's current pass
-    const int64_t lim = (int64_t)pd.bits_w * pd.m, span = 38ll * pd.m + 31ll * pd.n;
+    // windowed, w < 2048: per-lane store predicate (bits_lane_stored) for the
+    // rows of the lane's current pass; hi = (e + 7) m - R n, e = bit 0's column
+    const bool lwin = bits_lane_window(pd.bits_w);
+    const int64_t lim = (int64_t)pd.bits_w * pd.m, hlim = lim + 38ll * pd.m + 31ll * pd.n;
     int64_t negRn = -(int64_t)(32 * lane) * pd.n;
     unsigned* mb = a.mat + pd.mat_off + lane * 4;
     int q0 = 0, k0 = 0;  // lane 0 bit 0: chunk and pass of this super-block
@@ -723,7 +757,8 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
           sto = kw < nb && K >= blo;
           st = mb + ((int64_t)kw * nblk + (K - blo)) * 1024;
         }
-        const bool ls = !win || bits_lane_stored((int64_t)(eh + 7) * pd.m + negRn, lim, span);
+        bool ls = true;
+        if (lwin) ls = bits_lane_stored((int64_t)(eh + 7) * pd.m + negRn, lim, hlim);
         if (mask) {
           if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
           else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);

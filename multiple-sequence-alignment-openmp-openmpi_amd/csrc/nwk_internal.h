@@ -76,6 +76,12 @@ __host__ __device__ inline int bits_blk_lo(int b, int m, int n, int w) {
   return lo <= 0 ? 0 : (int)(lo >> 3);
 }
 
+// kBits / kBitsStrip windowed storage below one band's height: only the lane
+// words holding a cell within w columns of the diagonal are written (and the
+// traceback checks every cell against that); at w >= 2048 nearly every lane
+// word of a stored block holds such a cell, so all are written
+__host__ __device__ inline bool bits_lane_window(int w) { return w > 0 && w < kBitsRows; }
+
 // kBitsStrip: first stored 8-step block (strip step numbering) of band b's
 // window: its cells (i, j), |j - i n / m| <= w, sit at steps j + b np + (i - 2048 b)
 __host__ __device__ inline int strip_blk_lo(int b, int m, int n, int np, int w) {

@@ -1081,6 +1081,14 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         set_w(wc);
         return total_b();
       });
+    // Strips keep a 1024-column window even when full storage fits: below one
+    // band's height a window writes only the lane words near the diagonal
+    // (bits_lane_window), about half of them at 1024 -- C4's 8-rank shard
+    // fits in full, and full storage wrote ~6 TB/s of HBM at 4 waves/SIMD.
+    // Random 8k pairs' paths stay within ~400 columns (pathdev_c4.txt); a pair
+    // whose path leaves re-runs in full.  NWK_STRIP_WIN overrides (0: full).
+    static const int strip_win_env = getenv("NWK_STRIP_WIN") ? atoi(getenv("NWK_STRIP_WIN")) : 1024;
+    if (W == 0 && pl.mode == kBitsStrip) W = strip_win_env;
     set_w(W);
   }
   st.window = dp.empty() ? 0 : dp[0].bits_w;
