@@ -307,7 +307,7 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
   // columns of the diagonal (bits_lane_stored): dev = c m - i n of the current
   // cell (i = b 2048 + r), |dev| <= win m, else the path has left them
   int64_t dev = (int64_t)c * pd.m - (int64_t)(b * kBR + r) * pd.n;
-  const int64_t lim = (int64_t)win * pd.m, dD = (int64_t)pd.n - pd.m;
+  const int64_t lim = (int64_t)win * pd.m, dD = (int64_t)pd.n - pd.m, wmargin = 64 * ((int64_t)pd.m + pd.n);
   const bool lwin = bits_lane_window(win);
   if (lwin && c >= 0 && (dev > lim || dev < -lim)) out = true;
   while (!out && c >= 0 && (b > 0 || r >= 0)) {
@@ -326,6 +326,7 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
       break;
     }
     BITS_PROG(0x50000000u | ((unsigned)(Lc & 0xfff) << 16) | ((unsigned)(r & 0xff) << 8) | (unsigned)(c & 0xff));
+    if (Lc - flushed >= 192) flush(Lc & ~3);  // (the walk below adds <= 34 bytes + 63 junk to the 256-byte ring)
     if (b != tb || s > ts || s <= ts - 64 || (t != tt && t != tt - 1)) {
       tb = b;
       ts = s;
@@ -349,67 +350,59 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
     // j of the run is row r - j at lane L + 2 j, so every lane tests the cell
     // it holds, one ballot marks where the run stops and one find-first-set
     // gives its length.  The stopping cell's U / L move is read with one
-    // v_readlane, and the run plus that move go to the LDS ring in one masked
-    // store.  Random pairs' paths are ~80% D moves, so one iteration covers
-    // ~6 moves where the move-by-move walk spent ~50 instructions per move.
+    // v_readlane, and every lane writes one byte of the run and that move to
+    // the LDS ring (bytes past them are junk that the next iteration
+    // overwrites before any flush reads it).  Straight-line: one branch per
+    // iteration.  Random pairs' paths are ~70-80% D moves.
+    //
+    // Window: the cells reachable in this tile lie within 64 columns and 64
+    // rows of the current cell, so when it is that far inside the stored lane
+    // words (|dev| <= lim - 64 (m + n)) nothing in the tile needs a check.
+    const bool wchk = lwin && (dev > lim - wmargin || dev < -lim + wmargin);
     const int rowlo = tt > 0 ? 32 * (tt - 1) : 0;  // lowest row of the tile
     for (;;) {
-      if (lwin && (dev > lim || dev < -lim)) {  // this cell is outside the stored lane words
+      if (wchk && (dev > lim || dev < -lim)) {  // this cell is outside the stored lane words
         out = true;
         break;
       }
-      if (Lc - flushed >= 192) flush(Lc & ~3);  // (an iteration adds <= 33 bytes to the 256-byte ring)
       const int L = ts - s;  // lane of the current step
       // the run's cells j = 0 .. jmax are readable: in the tile's lanes and
       // rows, columns >= 0, stored steps (>= slo)
       int jmax = (63 - L) >> 1;
-      jmax = min(jmax, r - rowlo);
-      jmax = min(jmax, c);
-      jmax = min(jmax, (s - slo) >> 1);
+      const int jr = r - rowlo, js = (s - slo) >> 1;
+      jmax = jmax < jr ? jmax : jr;
+      jmax = jmax < c ? jmax : c;
+      jmax = jmax < js ? jmax : js;
       const int off = lane - L, jl = off >> 1, row = r - jl;
-      bool stop = false;
-      if (off >= 0 && !(off & 1) && jl <= jmax) {
-        const unsigned w = (row >> 5) == tt ? vd0 : vd1;
-        stop = ((w >> (row & 31)) & 1u) == 0u;
-      }
+      const unsigned w = (row >> 5) == tt ? vd0 : vd1;
+      const bool stop = off >= 0 && !(off & 1) && jl <= jmax && !((w >> (row & 31)) & 1u);
       const u64 stops = __builtin_amdgcn_ballot_w64(stop);
-      const int jn = stops ? (((int)__builtin_ctzll(stops) - L) >> 1) : jmax + 1;  // first non-D cell
-      if (lwin) {  // the run's cells (dev is linear along it: check its far end)
-        const int64_t de = dev + (int64_t)min(jn, jmax) * dD;
+      int jn = jmax + 1;  // D moves: cells 0 .. jn - 1 (jn <= jmax: cell jn stops the run)
+      if (stops) jn = ((int)__builtin_ctzll(stops) - L) >> 1;
+      const bool has = jn <= jmax;
+      if (wchk && dD != 0) {  // dev is linear along the run: check its far end
+        const int64_t de = dev + (int64_t)(has ? jn : jmax) * dD;
         if (de > lim || de < -lim) {
           out = true;
           break;
         }
       }
-      const int nD = jn;  // D moves (cells 0 .. jn - 1)
-      unsigned op = 0;
-      if (jn <= jmax) {  // the run stops on a readable cell: its move is U (v == 0) or L
-        const int rr = r - jn;
-        const unsigned uw = (rr >> 5) == tt ? vu0 : vu1;
-        const unsigned u = (unsigned)__builtin_amdgcn_readlane((int)uw, L + 2 * jn);
-        op = ((u >> (rr & 31)) & 1u) ? 'L' : 'U';
-      }
-      const int nw = nD + (op ? 1 : 0);
-      if (lane < nw)
-        asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((Lc + lane) & 255)), "v"(lane < nD ? 'D' : op)
-                     : "memory");
-      Lc += nw;
-      r -= nD;
-      c -= nD;
-      s -= 2 * nD;
-      dev += (int64_t)nD * dD;
-      if (op == 'U') {
-        --r;
-        s -= 1;
-        dev += pd.n;
-      } else if (op == 'L') {
-        --c;
-        s -= 1;
-        dev -= pd.m;
-      }
-      if (c < 0 || r < 0) break;
+      const int rr = r - jn;
+      const unsigned uw = (rr >> 5) == tt ? vu0 : vu1;
+      const unsigned u = (unsigned)__builtin_amdgcn_readlane((int)uw, has ? L + 2 * jn : 0);
+      const bool isU = has && !((u >> (rr & 31)) & 1u);  // U: v == 0, else L
+      const bool isL = has && !isU;
+      const unsigned op = isU ? 'U' : 'L';
+      asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((Lc + lane) & 255)), "v"(lane < jn ? 'D' : op)
+                   : "memory");
+      Lc += jn + (has ? 1 : 0);
+      r -= jn + (isU ? 1 : 0);
+      c -= jn + (isL ? 1 : 0);
+      s -= 2 * jn + (has ? 1 : 0);
+      dev += (int64_t)jn * dD + (isU ? (int64_t)pd.n : 0) - (isL ? (int64_t)pd.m : 0);
       const int t2 = r >> 5;
-      if (s <= ts - 64 || (t2 != tt && t2 != tt - 1) || s < slo) break;
+      if ((c < 0) | (r < 0) | (s <= ts - 64) | ((t2 != tt) & (t2 != tt - 1)) | (s < slo) | (Lc - flushed >= 192))
+        break;
     }
     if (out) break;
     if (Lc > pd.m + pd.n) {

@@ -107,11 +107,14 @@ __device__ __forceinline__ unsigned opaque_zero32() {
 // gives up after ~4 s of wall time (s_memrealtime runs at 100 MHz) or when
 // another wave has already failed, so a hand-off bug ends the grid instead of
 // hanging it; the caller tells success from the returned tags.
+#ifndef NWK_POLL_SLEEP
+#define NWK_POLL_SLEEP 4
+#endif
 __device__ __noinline__ u64 wait_granules(const u64* p, unsigned epoch, u64 v, unsigned* err) {
   const u64 t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     if (__all((unsigned)(v >> 32) == epoch)) return v;
-    __builtin_amdgcn_s_sleep(4);
+    __builtin_amdgcn_s_sleep(NWK_POLL_SLEEP);
     if (__hip_atomic_load((gu32*)err, RLX_AGENT) != 0u) return 0;
     if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
       if ((threadIdx.x & 63) == 0) atomicOr(err, 1u);

@@ -4,7 +4,7 @@
 set -euo pipefail
 cd "$(dirname "$0")/.."
 name=$1; shift
-out=tools/libvariants/$name
+out=${VARIANT_DIR:-tools/libvariants}/$name
 mkdir -p $out/obj
 P=multiple-sequence-alignment-openmp-openmpi_amd
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 $*"
