@@ -107,14 +107,30 @@ __device__ __forceinline__ unsigned opaque_zero32() {
 // gives up after ~4 s of wall time (s_memrealtime runs at 100 MHz) or when
 // another wave has already failed, so a hand-off bug ends the grid instead of
 // hanging it; the caller tells success from the returned tags.
-#ifndef NWK_POLL_SLEEP
-#define NWK_POLL_SLEEP 4
+// Each re-read below is a 64-lane atomic performed at the memory side, and
+// WRITE_SIZE counts it (nw_align_pka on 200k pairs: polls were ~1/3 of the
+// kernel's HBM writes, tools/pka_write_probe.py), so a wait backs off: the
+// sleep doubles from ~0.1 us to ~1.6 us (s_sleep n = 64 n cycles) -- a
+// 64-column chunk takes a band ~15 us, so the wait still ends within ~10%.
+#ifndef NWK_POLL_SLEEP_MAX
+#define NWK_POLL_SLEEP_MAX 32
 #endif
+__device__ __forceinline__ void poll_sleep(int& n) {
+  switch (n) {  // s_sleep takes an immediate
+    case 2: __builtin_amdgcn_s_sleep(2); break;
+    case 4: __builtin_amdgcn_s_sleep(4); break;
+    case 8: __builtin_amdgcn_s_sleep(8); break;
+    case 16: __builtin_amdgcn_s_sleep(16); break;
+    default: __builtin_amdgcn_s_sleep(NWK_POLL_SLEEP_MAX); break;
+  }
+  n = n < NWK_POLL_SLEEP_MAX ? 2 * n : n;
+}
 __device__ __noinline__ u64 wait_granules(const u64* p, unsigned epoch, u64 v, unsigned* err) {
   const u64 t0 = __builtin_amdgcn_s_memrealtime();
+  int nap = 2;
   for (;;) {
     if (__all((unsigned)(v >> 32) == epoch)) return v;
-    __builtin_amdgcn_s_sleep(NWK_POLL_SLEEP);
+    poll_sleep(nap);
     if (__hip_atomic_load((gu32*)err, RLX_AGENT) != 0u) return 0;
     if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
       if ((threadIdx.x & 63) == 0) atomicOr(err, 1u);

@@ -716,14 +716,26 @@ void parallel_for(int threads, int64_t n, F&& f) {
 struct Chain {
   const uint8_t* hashes = nullptr;  // [P][64] raw problem hashes
   std::vector<char> ready;
+  std::vector<uint64_t> kw;         // [P][80] second-block schedules (prepare), off the chain's critical path
+  std::vector<char> has_kw;
   int64_t next = 0;
   ChainAcc acc;  // acc starts as "" (skel:121)
+  void init(const uint8_t* h, int64_t P) {
+    hashes = h;
+    ready.assign((size_t)P, 0);
+    kw.assign((size_t)P * 80, 0);
+    has_kw.assign((size_t)P, 0);
+  }
+  // pair p's schedule (any thread, once its hash is written, before it is marked ready)
+  void prepare(int64_t p) {
+    chain_schedule(hashes + 64 * p, kw.data() + 80 * p);
+    has_kw[p] = 1;
+  }
   void advance() {
     const int64_t P = (int64_t)ready.size();
-    uint64_t kw[80];
     while (next < P && ready[next]) {
-      chain_schedule(hashes + 64 * next, kw);
-      chain_step(&acc, kw);
+      if (!has_kw[next]) prepare(next);
+      chain_step(&acc, kw.data() + 80 * next);
       ++next;
     }
   }
@@ -1643,6 +1655,10 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         memcpy(hashes + 64 * w.out, f.hash, 64);
       });
       if (chain) {  // serial: jobs never overlap each other (fin.join() before the next starts)
+        parallel_for(c->host_threads, (np + 255) / 256, [&](int64_t b) {  // second-block schedules, in parallel
+          for (int64_t q = b * 256; q < std::min<int64_t>(np, (b + 1) * 256); ++q)
+            if (!skipped(q)) chain->prepare(dw[q].out);
+        });
         for (int64_t q = 0; q < np; ++q)
           if (!skipped(q)) chain->ready[dw[q].out] = 1;
         chain->advance();
@@ -1753,8 +1769,7 @@ static int align_all_sc(nwk_ctx* c, const Scoring& sc, int32_t* penalties, uint8
   int rc = make_work(c, ids.data(), P, &w);
   if (rc != NWK_OK) return rc;
   Chain ch;
-  ch.hashes = problem_hash;
-  ch.ready.assign((size_t)P, 0);
+  ch.init(problem_hash, P);
   if ((rc = align_work(c, w, sc, penalties, problem_hash, nullptr, nullptr, &ch)) != NWK_OK) return rc;
   ch.advance();  // pairs with no DP cells, if they are the tail
   if (ch.next != P) return fail(NWK_EKERNEL, "nwk_align_all: chain stopped at pair %lld of %lld", (long long)ch.next, (long long)P);
@@ -1873,8 +1888,12 @@ int nwk_finalize_moves(const uint8_t* x, int32_t m, const uint8_t* y, int32_t n,
 int nwk_chain_hash(const uint8_t* ph, int64_t P, char* hash_hex) {
   if (!hash_hex || (P > 0 && !ph)) return fail(NWK_EINVAL, "nwk_chain_hash: bad argument");
   Chain ch;
-  ch.hashes = ph;
-  ch.ready.assign((size_t)std::max<int64_t>(P, 0), 1);
+  ch.init(ph, std::max<int64_t>(P, 0));
+  unsigned hc = std::thread::hardware_concurrency();
+  parallel_for((int)std::min(16u, hc ? hc : 1u), (P + 1023) / 1024, [&](int64_t b) {
+    for (int64_t p = b * 1024; p < std::min(P, (b + 1) * 1024); ++p) ch.prepare(p);
+  });
+  std::fill(ch.ready.begin(), ch.ready.end(), 1);
   ch.advance();
   ch.hex(hash_hex);
   return NWK_OK;
