@@ -260,13 +260,61 @@ __device__ __forceinline__ bool bits_lane_stored(int64_t hi, int64_t lim, int64_
   return hi >= -lim && hi <= hlim;  // hlim = w m + 38 m + 31 n: the span's low end <= w m
 }
 
-// Traceback of one pair from (m, n) over the stored (diag, up) bits.  A tile
-// is 64 steps (lane L holds step ts - L) of two row-lanes (tt and tt - 1),
-// four dwords per lane; the walk goes by diagonal runs (see the loop).
+// Traceback of one pair from (m, n) over the stored (diag, up) bits.
+//
+// Tiles are 64 steps (grid-aligned: ts = s | 63; lane L holds step ts - L) by
+// four row-lanes ta .. ta - 3 (128 rows; the current row is in ta or below),
+// eight dwords per lane.  While the walk crosses one tile, the next one along
+// the steps (ts - 64, anchored at the row-lane the walk entered with) is
+// already loading.
+//
+// Inside a tile the walk runs on the scalar unit over 64-bit lane masks.  A
+// D move goes from (row r, lane L) to (r - 1, L + 2), so every cell of a
+// diagonal run has the same key K = r + (L >> 1) and lies on lanes of L's
+// parity.  Each lane re-indexes its column of bits by key (a per-lane funnel
+// shift, once per tile): then one ballot per key gives, for every lane at
+// once, whether its cell on that key's diagonal is a D move (Dm) or an UP
+// move (Um).  A run from (L, K) stops at the first lane >= L of L's parity
+// whose Dm bit is clear; that cell moves U or L as Um says, and the next run
+// starts one lane on, at key K + (L & 1) - [U].  A run costs ~20 scalar
+// instructions and two ballots only when its key is new, instead of a vector
+// round trip per run.  The moves of a tile are written once, when it is left:
+// lanes visited in lane order, each at its rank among the visited lanes
+// (v_mbcnt), through a 1 KB LDS ring flushed to ops[].
 #define BITS_PROG(v)                                                                                         \
   do {                                                                                                       \
     if (prog && lane == 0) __hip_atomic_store((gu32*)prog, (unsigned)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); \
   } while (0)
+
+// scalar min (the compiler would take v_min3 and a readfirstlane round trip)
+__device__ __forceinline__ int smin(int a, int b) {
+  int r;
+  asm("s_min_i32 %0, %1, %2" : "=s"(r) : "s"(__builtin_amdgcn_readfirstlane(a)), "s"(__builtin_amdgcn_readfirstlane(b)) : "scc");
+  return r;
+}
+
+__device__ __forceinline__ int sminu(int a, int b) {
+  int r;
+  asm("s_min_u32 %0, %1, %2" : "=s"(r) : "s"(__builtin_amdgcn_readfirstlane(a)), "s"(__builtin_amdgcn_readfirstlane(b)) : "scc");
+  return r;
+}
+// first set bit of a 64-bit mask, -1 when none
+__device__ __forceinline__ int sff1(u64 m) {
+  int r;
+  asm("s_ff1_i32_b64 %0, %1" : "=s"(r) : "s"(m) : "scc");
+  return r;
+}
+
+#ifndef NWK_TRACE_PROF
+#define NWK_TRACE_PROF 0  // 1: the timeline's trace columns become a cycle breakdown (A/B only)
+#endif
+constexpr int kTraceRing = 1024;  // bytes of LDS per wave for the trace's move ring
+#ifndef NWK_TRACE_NB
+#define NWK_TRACE_NB 3  // step-tiles per prefetched batch
+#endif
+constexpr int kNB = NWK_TRACE_NB;
+// s_waitcnt immediate for vmcnt(n) leaving expcnt / lgkmcnt alone (gfx9 encoding)
+constexpr int waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0F70; }
 
 // NWK_TRACE_PRIO 1: the traceback wave raises its issue priority (s_setprio 3)
 #ifndef NWK_TRACE_PRIO
@@ -292,7 +340,8 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
     const int from = flushed & ~3;
     for (int o = from + 4 * lane; o < upto; o += 256) {
       unsigned v;
-      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ob + (unsigned)(o & 255)) : "memory");
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ob + (unsigned)(o & (kTraceRing - 1)))
+                   : "memory");
       *reinterpret_cast<unsigned*>(ops + o) = v;
     }
     flushed = upto;
@@ -300,110 +349,305 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
   // position: band b, band row r (0..2047, -1 = the row above the band), column c (0-based)
   int b = (pd.m - 1) / kBR, r = (pd.m - 1) % kBR, c = pd.n - 1;
   if (a.dbg_notrace) c = -1;  // NWK_NOTRACE (fill timing): no moves, the walk "ends" at (m, n)
-  int tb = -1, ts = 0, tt = 0, blo = 0, slo = 0;
-  unsigned vd0 = 0, vu0 = 0, vd1 = 0, vu1 = 0;
+  int tb = -1, ts = 0, ta = 0, blo = 0, slo = 0;
+  unsigned vd[4] = {0, 0, 0, 0}, vu[4] = {0, 0, 0, 0};
+  // Tiles come in batches of kNB consecutive step-tiles: tile j of a batch
+  // covers steps bts - 64 j - 63 .. bts - 64 j, row-lanes bpa[j] .. bpa[j] - 3
+  // (anchored where the walk is predicted to enter it).  The walk crosses the
+  // current batch (c*) while the next one (n*) is in flight; the next batch's
+  // registers are read only after everything has arrived, so the compiler's
+  // waits never stall the walk on it.  A tile is eight loads with addresses
+  // clamped into the band's storage (cells off the stored steps or above row
+  // 0 are never read: the walk's jmax excludes them).
+  unsigned cd[kNB][4], cu[kNB][4], nd[kNB][4], nu[kNB][4];
+  int cts = -1, cb = -1, cpa[kNB], nts = -1, nbb = -1, npa[kNB];
+#pragma unroll
+  for (int j = 0; j < kNB; ++j) cpa[j] = npa[j] = 0;
+  // rows per step along the pair (16.16): predicts the row a tile ahead is entered at
+  const int64_t slope = ((int64_t)pd.m << 16) / ((int64_t)pd.m + pd.n);
+  auto load_tile = [&](int ts_, int ta_, unsigned (&d)[4], unsigned (&u)[4]) {
+    int sl = ts_ - lane;
+    int rel = (sl >> 3) - blo;
+    const bool okl = sl >= 0 && (unsigned)rel < (unsigned)nblk;
+    sl = okl ? sl : 0;
+    rel = okl ? rel : 0;
+    const unsigned* p0 =
+        mat + (sfull ? 0 : (int64_t)b * bdw) + (int64_t)rel * 1024 + ((sl & 7) >> 2) * 256 + (sl & 3);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int rl = ta_ - k < 0 ? 0 : ta_ - k;
+      d[k] = __builtin_nontemporal_load(p0 + 4 * rl);
+      u[k] = __builtin_nontemporal_load(p0 + 512 + 4 * rl);
+    }
+  };
+  // row-lane anchor of the tile k tiles ahead: the walk at (r, lane L) reaches
+  // its top step after 64 k - L steps, ~slope rows per step; 24 rows of slack above
+  auto predict = [&](int k, int L) {
+    const int rp = r - (int)(((int64_t)(64 * k - L) * slope) >> 16);
+    const int pa = (rp + 24) >> 5;
+    return pa < 0 ? 0 : (pa > kBR / 32 - 1 ? kBR / 32 - 1 : pa);
+  };
   bool bad = false, out = false;
+  // verbose >= 2 timeline: walk cycles, runs, tiles entered, batches loaded (demand / ahead)
+  const u64 tc0 = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+  unsigned n_runs = 0, n_tiles = 0, n_dem = 0, n_ahead = 0;
+#if NWK_TRACE_PROF
+  u64 p_sw = 0, p_win = 0, p_walk = 0, p_out = 0, p_wait = 0, p_nb = 0;
+#endif
   // windowed storage keeps only the lane words holding a cell within win
   // columns of the diagonal (bits_lane_stored): dev = c m - i n of the current
   // cell (i = b 2048 + r), |dev| <= win m, else the path has left them
-  int64_t dev = (int64_t)c * pd.m - (int64_t)(b * kBR + r) * pd.n;
   const int64_t lim = (int64_t)win * pd.m, dD = (int64_t)pd.n - pd.m, wmargin = 64 * ((int64_t)pd.m + pd.n);
   const bool lwin = bits_lane_window(win);
-  if (lwin && c >= 0 && (dev > lim || dev < -lim)) out = true;
+  auto devof = [&]() { return (int64_t)c * pd.m - (int64_t)(b * kBR + r) * pd.n; };
+  if (lwin && c >= 0) {
+    const int64_t dev = devof();
+    if (dev > lim || dev < -lim) out = true;
+  }
+  constexpr u64 kEven = 0x5555555555555555ull;
   while (!out && c >= 0 && (b > 0 || r >= 0)) {
     if (r < 0) {  // into the band above
       --b;
       r += kBR;
     }
-    int t = r >> 5;
+    const int t = r >> 5;
     int s = c + r + (snp > 0 ? b * snp : 0);
     if (b != tb) {
       blo = snp > 0 ? strip_blk_lo(b, pd.m, pd.n, snp, win) : bits_blk_lo(b, pd.m, pd.n, win);
+      blo = __builtin_amdgcn_readfirstlane(blo);  // (uniform: keep the walk's bounds in SGPRs)
       slo = 8 * blo;  // lowest stored step of band b
     }
     if ((unsigned)((s >> 3) - blo) >= (unsigned)nblk) {  // the path left the stored window
       out = true;
       break;
     }
+#if NWK_TRACE_PROF
+    const u64 pt0 = __builtin_amdgcn_s_memtime();
+#endif
     BITS_PROG(0x50000000u | ((unsigned)(Lc & 0xfff) << 16) | ((unsigned)(r & 0xff) << 8) | (unsigned)(c & 0xff));
-    if (Lc - flushed >= 192) flush(Lc & ~3);  // (the walk below adds <= 34 bytes + 63 junk to the 256-byte ring)
-    if (b != tb || s > ts || s <= ts - 64 || (t != tt && t != tt - 1)) {
-      tb = b;
-      ts = s;
-      tt = t;
-      const int sl = s - lane;
-      const int rel = (sl >> 3) - blo;
-      vd0 = vu0 = vd1 = vu1 = 0;
-      if (sl >= 0 && (unsigned)rel < (unsigned)nblk) {
-        const unsigned* p0 = mat + (sfull ? 0 : (int64_t)b * bdw) + (int64_t)rel * 1024 + ((sl & 7) >> 2) * 256 +
-                             t * 4 + (sl & 3);
-        vd0 = __builtin_nontemporal_load(p0);
-        vu0 = __builtin_nontemporal_load(p0 + 512);
-        if (t > 0) {
-          vd1 = __builtin_nontemporal_load(p0 - 4);
-          vu1 = __builtin_nontemporal_load(p0 + 508);
+    if (Lc - flushed >= kTraceRing - 128) flush(Lc & ~3);  // (a tile adds <= 64 moves to the ring)
+    if (b != tb || s > ts || s <= ts - 64 || t > ta || t < ta - 3) {
+      const int sg = s | 63;
+      int j = (cts - sg) >> 6;
+      if (!(b == cb && sg <= cts && j < kNB && t <= cpa[j] && t >= cpa[j] - 3)) {  // not in the current batch
+        const int jn = (nts - sg) >> 6;
+        if (!(b == nbb && sg <= nts && jn < kNB && t <= npa[jn] && t >= npa[jn] - 3)) {
+          // nor in the next one: load the batch starting at this tile
+          ++n_dem;
+          nts = sg;
+          nbb = b;
+#pragma unroll
+          for (int i = 0; i < kNB; ++i) {
+            npa[i] = i == 0 ? t : predict(i, sg - s);
+            load_tile(nts - 64 * i, npa[i], nd[i], nu[i]);
+          }
+        }
+#if NWK_TRACE_PROF
+        const u64 pw0 = __builtin_amdgcn_s_memtime();
+#endif
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+#if NWK_TRACE_PROF
+        p_wait += __builtin_amdgcn_s_memtime() - pw0;
+        ++p_nb;
+#endif
+        cts = nts;
+        cb = nbb;
+#pragma unroll
+        for (int i = 0; i < kNB; ++i) {
+          cpa[i] = npa[i];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            cd[i][k] = nd[i][k];
+            cu[i][k] = nu[i][k];
+          }
+        }
+        j = (cts - sg) >> 6;
+        // the batch after it goes out now
+        nts = cts - 64 * kNB;
+        nbb = nts >= slo ? b : -1;
+        if (nbb >= 0) {
+          ++n_ahead;
+#pragma unroll
+          for (int i = 0; i < kNB; ++i) {
+            npa[i] = predict(kNB + i - j, sg - s);
+            load_tile(nts - 64 * i, npa[i], nd[i], nu[i]);
+          }
         }
       }
-    }
-    // Walk inside the tile by diagonal runs.  From the current cell (row r,
-    // lane L = ts - s) the path takes D moves while the diag bit is set: cell
-    // j of the run is row r - j at lane L + 2 j, so every lane tests the cell
-    // it holds, one ballot marks where the run stops and one find-first-set
-    // gives its length.  The stopping cell's U / L move is read with one
-    // v_readlane, and every lane writes one byte of the run and that move to
-    // the LDS ring (bytes past them are junk that the next iteration
-    // overwrites before any flush reads it).  Straight-line: one branch per
-    // iteration.  Random pairs' paths are ~70-80% D moves.
-    //
-    // Window: the cells reachable in this tile lie within 64 columns and 64
-    // rows of the current cell, so when it is that far inside the stored lane
-    // words (|dev| <= lim - 64 (m + n)) nothing in the tile needs a check.
-    const bool wchk = lwin && (dev > lim - wmargin || dev < -lim + wmargin);
-    const int rowlo = tt > 0 ? 32 * (tt - 1) : 0;  // lowest row of the tile
-    for (;;) {
-      if (wchk && (dev > lim || dev < -lim)) {  // this cell is outside the stored lane words
-        out = true;
-        break;
+      ts = __builtin_amdgcn_readfirstlane(cts - 64 * j);
+      {
+        int pa = cpa[0];
+#pragma unroll
+        for (int i = 1; i < kNB; ++i) pa = j == i ? cpa[i] : pa;
+        ta = __builtin_amdgcn_readfirstlane(pa);
       }
-      const int L = ts - s;  // lane of the current step
-      // the run's cells j = 0 .. jmax are readable: in the tile's lanes and
-      // rows, columns >= 0, stored steps (>= slo)
-      int jmax = (63 - L) >> 1;
-      const int jr = r - rowlo, js = (s - slo) >> 1;
-      jmax = jmax < jr ? jmax : jr;
-      jmax = jmax < c ? jmax : c;
-      jmax = jmax < js ? jmax : js;
-      const int off = lane - L, jl = off >> 1, row = r - jl;
-      const unsigned w = (row >> 5) == tt ? vd0 : vd1;
-      const bool stop = off >= 0 && !(off & 1) && jl <= jmax && !((w >> (row & 31)) & 1u);
-      const u64 stops = __builtin_amdgcn_ballot_w64(stop);
-      int jn = jmax + 1;  // D moves: cells 0 .. jn - 1 (jn <= jmax: cell jn stops the run)
-      if (stops) jn = ((int)__builtin_ctzll(stops) - L) >> 1;
-      const bool has = jn <= jmax;
-      if (wchk && dD != 0) {  // dev is linear along the run: check its far end
-        const int64_t de = dev + (int64_t)(has ? jn : jmax) * dD;
-        if (de > lim || de < -lim) {
-          out = true;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        unsigned dd = cd[0][k], uu = cu[0][k];
+#pragma unroll
+        for (int i = 1; i < kNB; ++i) {
+          dd = j == i ? cd[i][k] : dd;
+          uu = j == i ? cu[i][k] : uu;
+        }
+        vd[k] = dd;
+        vu[k] = uu;
+      }
+      tb = b;
+      ++n_tiles;
+    }
+#if NWK_TRACE_PROF
+    const u64 pt1 = __builtin_amdgcn_s_memtime();
+    p_sw += pt1 - pt0;
+#endif
+    // Key window: keys Kb .. Kb + 31 around the entry key.  Lane l's bit i is
+    // its cell at row Kb + i - (l >> 1): bit q = that row - 32 (ta - 3) + 32 of
+    // the column {0, vd[3], vd[2], vd[1], vd[0], 0} (rows outside the tile read 0).
+    int L = ts - s;
+    const int Kb = r + (L >> 1) - 20;
+    const int rowlo = ta > 3 ? 32 * (ta - 3) : 0;  // lowest row of the tile
+    unsigned WD, WU;
+    {
+      const int q = Kb - (lane >> 1) - 32 * (ta - 3) + 32;
+      const int dq = q >> 5, sh = q & 31;
+      const bool ok = q >= 0 && q < 160;
+      const unsigned dlo = dq == 1 ? vd[3] : dq == 2 ? vd[2] : dq == 3 ? vd[1] : dq == 4 ? vd[0] : 0u;
+      const unsigned dhi = dq == 0 ? vd[3] : dq == 1 ? vd[2] : dq == 2 ? vd[1] : dq == 3 ? vd[0] : 0u;
+      const unsigned ulo = dq == 1 ? vu[3] : dq == 2 ? vu[2] : dq == 3 ? vu[1] : dq == 4 ? vu[0] : ~0u;
+      const unsigned uhi = dq == 0 ? vu[3] : dq == 1 ? vu[2] : dq == 2 ? vu[1] : dq == 3 ? vu[0] : ~0u;
+      WD = ok ? __builtin_amdgcn_alignbit(dhi, dlo, sh) : 0u;
+      WU = ok ? __builtin_amdgcn_alignbit(uhi, ulo, sh) : ~0u;  // stored up word: 0 = UP
+    }
+#if NWK_TRACE_PROF
+    const u64 pt2 = __builtin_amdgcn_s_memtime();
+    p_win += pt2 - pt1;
+#endif
+    const bool wchk = lwin && [&] {
+      const int64_t dev = devof();
+      return dev > lim - wmargin || dev < -lim + wmargin;
+    }();
+    u64 vD = 0, vU = 0, vL = 0;  // lanes visited by D / U / L moves in this tile
+    // The run loop, all scalar; a second copy checks the stored lane words
+    // (windowed storage, only in tiles near the window's edge).
+    auto walk = [&](auto chk) {
+      constexpr bool kChk = decltype(chk)::value;
+      int Kc = -(1 << 30);
+      u64 Dm = 0, Um = 0;
+      for (;;) {
+        if constexpr (kChk) {  // this cell must be inside the stored lane words
+          const int64_t dev = devof();
+          if (dev > lim || dev < -lim) {
+            out = true;
+            return;
+          }
+        }
+        if (a.stamps) ++n_runs;
+        const int K = r + (L >> 1);
+        if (K != Kc) {
+          const int i = K - Kb;
+          if ((unsigned)i > 31u) return;  // off the key window: re-window (same tile)
+          Dm = __builtin_amdgcn_ballot_w64((WD >> i) & 1u);
+          Um = __builtin_amdgcn_ballot_w64(!((WU >> i) & 1u));
+          Kc = K;
+        }
+        // the run's cells j = 0 .. jmax are readable: in the tile's lanes and
+        // rows, columns >= 0, stored steps (>= slo)
+        const int jmax = smin(smin((63 - L) >> 1, r - rowlo), smin(c, (s - slo) >> 1));
+        const u64 par = (L & 1) ? ~kEven : kEven;
+        const u64 stops = ~Dm & par & (~0ull << L);
+        const int lend = L + 2 * jmax + 2;  // first lane past the readable cells
+        const int ls = min(stops ? (int)__builtin_ctzll(stops) : lend, lend);
+        const int jn = (ls - L) >> 1;  // D moves: cells 0 .. jn - 1
+        if constexpr (kChk) {
+          if (dD != 0) {  // dev is linear along the run: check its far end
+            const int64_t de = devof() + (int64_t)(ls < lend ? jn : jmax) * dD;
+            if (de > lim || de < -lim) {
+              out = true;
+              return;
+            }
+          }
+        }
+        vD |= par & (ls >= 64 ? ~0ull : ((1ull << ls) - 1)) & (~0ull << L);
+        r -= jn;
+        c -= jn;
+        s -= 2 * jn;
+        if (ls >= lend) return;  // the run leaves the tile
+        // cell jn stops the run: U or L
+        const u64 bit = 1ull << ls;
+        const int u = (Um & bit) ? 1 : 0;
+        vU |= u ? bit : 0ull;
+        vL |= u ? 0ull : bit;
+        r -= u;
+        c -= 1 - u;
+        s -= 1;
+        L = ls + 1;
+        if ((L > 63) | (c < 0) | (r < rowlo) | (s < slo)) return;
+      }
+    };
+    if (wchk) {
+      walk(std::true_type{});
+    } else {
+      // The common case, ~35 scalar instructions a run: lanes past the stored
+      // steps are cut by one per-tile bound (LL), rows and columns by jb; the D
+      // lanes are not collected per run but rebuilt once from the stops below.
+      const int LL = smin(63, ts - slo);  // last lane whose step is stored
+      const int L0 = L;
+      u64 vS = 0;  // lanes of the runs' stopping cells (U or L moves)
+      int Kc = -(1 << 30);
+      u64 Dm = 0, Um = 0;
+      for (;;) {
+        const int jb = smin(r - rowlo, c);  // cells j <= jb keep row >= rowlo, column >= 0
+        if ((jb < 0) | (L > LL)) break;     // the current cell is outside the tile
+        ++n_runs;
+        const int K = r + (L >> 1);
+        if (K != Kc) {
+          const int i = K - Kb;
+          if ((unsigned)i > 31u) break;  // off the key window: re-window (same tile)
+          Dm = __builtin_amdgcn_ballot_w64((WD >> i) & 1u);
+          Um = __builtin_amdgcn_ballot_w64(!((WU >> i) & 1u));
+          Kc = K;
+        }
+        const int lend = L + 2 * smin(jb, (LL - L) >> 1) + 2;  // first lane past the readable cells
+        const u64 stops = ~Dm & ((L & 1) ? ~kEven : kEven) & (~0ull << L);
+        const int ls = sminu(sff1(stops), lend);  // (no stop: ff1 = -1)
+        const int jn = (ls - L) >> 1;
+        r -= jn;
+        c -= jn;
+        if (ls >= lend) {  // the run leaves the tile
+          L = ls;
           break;
         }
+        const u64 bit = 1ull << ls;
+        vS |= bit;
+        const int u = (Um & bit) ? 1 : 0;
+        vU |= u ? bit : 0ull;
+        r -= u;
+        c -= 1 - u;
+        L = ls + 1;
       }
-      const int rr = r - jn;
-      const unsigned uw = (rr >> 5) == tt ? vu0 : vu1;
-      const unsigned u = (unsigned)__builtin_amdgcn_readlane((int)uw, has ? L + 2 * jn : 0);
-      const bool isU = has && !((u >> (rr & 31)) & 1u);  // U: v == 0, else L
-      const bool isL = has && !isU;
-      const unsigned op = isU ? 'U' : 'L';
-      asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((Lc + lane) & 255)), "v"(lane < jn ? 'D' : op)
-                   : "memory");
-      Lc += jn + (has ? 1 : 0);
-      r -= jn + (isU ? 1 : 0);
-      c -= jn + (isL ? 1 : 0);
-      s -= 2 * jn + (has ? 1 : 0);
-      dev += (int64_t)jn * dD + (isU ? (int64_t)pd.n : 0) - (isL ? (int64_t)pd.m : 0);
-      const int t2 = r >> 5;
-      if ((c < 0) | (r < 0) | (s <= ts - 64) | ((t2 != tt) & (t2 != tt - 1)) | (s < slo) | (Lc - flushed >= 192))
-        break;
+      // D lanes: in [L0, L), not a stop, an even offset from the start of their run
+      const u64 starts = (1ull << L0) | (vS << 1);
+      const u64 sb = (starts & ((2ull << lane) - 1)) | 1ull;
+      const int a0 = 63 - __builtin_clzll(sb);
+      vD = __builtin_amdgcn_ballot_w64(lane >= L0 && lane < L && !((vS >> lane) & 1u) && !((lane - a0) & 1));
+      vL = vS & ~vU;
     }
+#if NWK_TRACE_PROF
+    const u64 pt3 = __builtin_amdgcn_s_memtime();
+    p_walk += pt3 - pt2;
+#endif
+    // the tile's moves, in lane order, into the ring
+    {
+      const u64 vis = vD | vU | vL;
+      const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(vis >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)vis, 0u));
+      const unsigned ch = ((vU >> lane) & 1u) ? 'U' : ((vL >> lane) & 1u) ? 'L' : 'D';
+      if ((vis >> lane) & 1u)
+        asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((Lc + (int)rank) & (kTraceRing - 1))), "v"(ch)
+                     : "memory");
+      Lc += __builtin_popcountll(vis);
+    }
+#if NWK_TRACE_PROF
+    p_out += __builtin_amdgcn_s_memtime() - pt3;
+#endif
     if (out) break;
     if (Lc > pd.m + pd.n) {
       bad = true;
@@ -411,6 +655,19 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
     }
   }
   if (bad && lane == 0) atomicOr(a.err, 16u);
+  if (a.stamps && lane == 0) {
+    u64* x = a.stamps + 8 * pd.slot;
+    x[2] = __builtin_amdgcn_s_memtime() - tc0;
+#if NWK_TRACE_PROF
+    x[3] = p_sw;
+    x[4] = p_walk;
+    x[5] = (p_wait << 32) | p_nb;
+#else
+    x[3] = n_runs;
+    x[4] = (u64)Lc;
+    x[5] = ((u64)n_tiles << 32) | ((u64)n_dem << 16) | n_ahead;
+#endif
+  }
   flush(Lc);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0) {
@@ -437,7 +694,7 @@ template <int NP, int SR>
 __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned cons_all[4][64 * NP];
   __shared__ __attribute__((aligned(16))) unsigned ring_all[4][128 * NP];
-  __shared__ __attribute__((aligned(16))) unsigned char obuf_all[4][256];
+  __shared__ __attribute__((aligned(16))) unsigned char obuf_all[4][kTraceRing];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   unsigned* prog = a.prog ? a.prog + blockIdx.x * 4 + wid : nullptr;  // NWK_WATCHDOG markers
@@ -643,7 +900,7 @@ template <int NP, int SR>
 __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned cons_all[4][64 * NP];
   __shared__ __attribute__((aligned(16))) unsigned ring_all[4][128 * NP];
-  __shared__ __attribute__((aligned(16))) unsigned char obuf_all[4][256];
+  __shared__ __attribute__((aligned(16))) unsigned char obuf_all[4][kTraceRing];
   extern __shared__ __attribute__((aligned(16))) unsigned hand_all[];  // [4][a.strip_ring]
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;

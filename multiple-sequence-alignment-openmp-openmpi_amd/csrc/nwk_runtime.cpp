@@ -1528,7 +1528,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         fprintf(stderr, "\n");
       }
       fprintf(stderr, "nwk timeline (ms after first pair filled; kernel %.3f ms): pair m x n: filled -> traced | "
-                      "trace cycles switch/blocks, blocks, switches/walk-cycles | fill band-cycles, %% waiting on band above\n", ms);
+                      "trace cycles, runs, moves, tiles/(demand batches << 16 | ahead batches) | fill band-cycles, %% waiting on band above\n", ms);
       double bc = 0, wc = 0;
       for (int q = 0; q < np; ++q) {
         const unsigned long long* x = &sp[8 * q];
