@@ -139,8 +139,18 @@ __device__ __noinline__ u64 wait_granules(const u64* p, unsigned epoch, u64 v, u
     // Re-read through an atomic: it is performed at the coherence point, so a
     // stale copy of the line in this XCD's L2 (left by the first, too-early
     // load) cannot keep the poll spinning.  The tag makes any copy safe to
-    // USE; only liveness needs the coherent re-read.
-    v = __hip_atomic_fetch_add((gu64*)p, opaque_zero64(), RLX_AGENT);
+    // USE; only liveness needs the coherent re-read.  A chunk's granules are
+    // published by one 64-lane store, so only the first stale lane polls (a
+    // sentinel, 8 bytes instead of 512 per poll); once it has arrived every
+    // stale lane re-reads.
+    const int lane = threadIdx.x & 63;
+    const u64 stale = __ballot((unsigned)(v >> 32) != epoch);
+    const int l = __builtin_ctzll(stale);
+    u64 pv = 0;
+    if (lane == l) pv = __hip_atomic_fetch_add((gu64*)p, opaque_zero64(), RLX_AGENT);
+    if ((unsigned)__builtin_amdgcn_readlane((int)(pv >> 32), l) == epoch) {
+      if ((stale >> lane) & 1ull) v = __hip_atomic_fetch_add((gu64*)p, opaque_zero64(), RLX_AGENT);
+    }
   }
 }
 

@@ -847,7 +847,7 @@ int align_linear_batch(nwk_ctx* c, const Plan& pl0, const Scoring& sc, const Pai
     for (int q = 0; q < np; ++q) fprintf(stderr, " %lld", (long long)ws[q].id);
     fprintf(stderr, "\n");
   }
-  FillArgs fa;
+  FillArgs fa{};
   memset(&fa, 0, sizeof fa);
   fa.pairs = c->d_pairs.as<PairDesc>();
   fa.tasks = c->d_tasks.as<int2>();
@@ -1363,7 +1363,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       HIP_TRY(hipMemsetAsync(c->d_segctl.p, 0, (size_t)segctl_b, c->stream));
     }
 
-    FillArgs fa;
+    FillArgs fa{};
     fa.pairs = c->d_pairs.as<PairDesc>();
     fa.tasks = c->d_tasks.as<int2>();
     fa.ntasks = (int)ntasks;
@@ -2332,7 +2332,7 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
     HIP_TRY(hipMemcpyAsync(d_tk.p, tk.data(), sizeof(int2) * ntasks, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(c->d_ctl.p, 0, 256, c->stream));
     HIP_TRY(hipMemsetAsync(c->d_done.p, 0, sizeof(unsigned) * np, c->stream));
-    FillArgs fa;
+    FillArgs fa{};
     memset(&fa, 0, sizeof fa);
     fa.pairs = d_pd.as<PairDesc>();
     fa.tasks = d_tk.as<int2>();
