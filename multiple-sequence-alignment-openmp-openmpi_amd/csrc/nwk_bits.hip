@@ -666,9 +666,9 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
   if (a.stamps && lane == 0) {
     u64* x = a.stamps + 8 * pd.slot;
     x[2] = __builtin_amdgcn_s_memtime() - tc0;
-#if NWK_TRACE_PROF
-    x[3] = p_sw;
-    x[4] = p_walk;
+#if NWK_TRACE_PROF  // {tile switch | key window} {walk | move output} {load wait | batches} cycles
+    x[3] = (p_sw << 32) | p_win;
+    x[4] = (p_walk << 32) | p_out;
     x[5] = (p_wait << 32) | p_nb;
 #else
     x[3] = n_runs;

@@ -109,10 +109,12 @@ def chunk_parts(lengths, rank, world, chunks):
 
 
 def auto_chunks(P, world):
-    """Pieces per rank: the chain of skel:159 costs ~0.25 us per link on the
-    host, so jobs of many pairs (C4: 32,640) hide all but the last piece's
-    links behind the alignment; small jobs keep one piece (one launch)."""
-    return 2 if P >= 8192 and world > 1 else 1
+    """Pieces per rank: one.  A piece's pairs finish together at the end of its
+    launch (strips: one wave per pair, one round), and a half-full launch takes
+    as long as a full one, so two pieces cost a second fill: C4 at W = 8, 1
+    piece 28.4 ms, 2 pieces 31.0 ms (profiles/r03/sched).
+    align_sharded_pipelined keeps the piece machinery for chunks > 1."""
+    return 1
 
 
 def align_sharded_pipelined(eng, lengths, pxy, pgap, rank, world, chunks=1, device=None, group=None,

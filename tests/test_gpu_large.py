@@ -6,10 +6,11 @@ and tests/golden/gen_inputs.py):
   c3.json                  answer hash + all penalties from oracle/_ref/sub, the
                            reference's own submitted program, on the full config
                            (the reference's evidence model: testing3/sequential.txt:2-3)
-  c4.json                  the same from the oracle's C restatement (nw_oracle.c, 8
-                           processes): sub's singleton rank takes ~1 s per 8k pair
-                           here (~9 h for 32,640 pairs); the generator asserts the
-                           oracle's first 36 problemhashes equal skel_debug's
+  c4.json                  the same from oracle/_ref/skel_debug, the reference's own
+                           skeleton, every pair as a two-sequence job (6 processes,
+                           3,538 s): the answer is skel:159's chain over its 32,640
+                           per-pair problemhashes (all equal to the oracle
+                           restatement's); sub's singleton rank would need ~9 h
   c3_pairs / c4_pairs      per-pair penalty + problemhash of the first 36 canonical
                            pairs from skel_debug (skel:158-169)
   c5_scores.json           affine go=3 ge=1 (and linear) penalties of pairs 0 and 1
