@@ -375,7 +375,13 @@ def main():
     lengths = [len(g) for g in genes]
     total_cells = workloads.cells(genes)
     ws = int(float(os.environ.get("NWK_BENCH_WS_GB", "0")) * (1 << 30))  # test hook: per-rank HBM budget
-    eng = seqalign.Engine(device=gpu, bits=args.bits, verbose=args.verbose, workspace_bytes=ws)
+    # sharded linear jobs of many pairs (C4: 32,640, a ~14 ms chain on rank 0):
+    # one launch per rank whose records stream out as pairs are hashed inside
+    # the fill launch (finalize "fused"), pieces of canonical ids exchanged and
+    # chained as they complete (C4 at 8 ranks: 24.3 ms vs 28.4 ms)
+    stream = sharded and not affine and int(os.environ.get("NWK_BENCH_STREAM", "1" if P >= 8192 else "0")) == 1
+    eng = seqalign.Engine(device=gpu, bits=args.bits, verbose=args.verbose, workspace_bytes=ws,
+                          finalize="fused" if stream else "auto")
     eng.set_sequences(genes)  # sequences resident in HBM before timing
     my_ids = seqalign.shard_pairs(lengths, rank, world) if sharded else np.arange(P, dtype=np.int64)
 
@@ -387,12 +393,16 @@ def main():
 
     # sharded linear runs: the shard in `chunks` pieces, each piece's records
     # all-gathered (and chained on rank 0) while the next piece aligns
-    chunks = int(os.environ.get("NWK_BENCH_CHUNKS", "0")) or nwdist_auto_chunks(P, world)
+    chunks = int(os.environ.get("NWK_BENCH_CHUNKS", "0")) or (16 if stream else nwdist_auto_chunks(P, world))
     piece_stats = []
 
     def step():
         del piece_stats[:]
-        if sharded and not affine:
+        if stream:
+            h, pen, _ = nwdist.align_sharded_streamed(eng, lengths, pxy, pgap, rank, world, chunks=chunks,
+                                                      device=coll_device)
+            piece_stats.append(eng.stats())  # (the call has ended inside)
+        elif sharded and not affine:
             h, pen, _ = nwdist.align_sharded_pipelined(eng, lengths, pxy, pgap, rank, world, chunks=chunks,
                                                        device=coll_device,
                                                        on_piece=lambda c: piece_stats.append(eng.stats()))
@@ -476,7 +486,9 @@ def main():
         "config": {"workload": name, "pairs": P, "cells": total_cells, "pxy": pxy,
                    "gaps": ("affine go=%d ge=%d" % (go, ge)) if affine else "linear pgap=%d" % pgap,
                    "storage_bits_per_cell": st["bits"], "mode": seqalign.MODES.get(st["mode"]),
-                   "parallelism": "pair-sharded dp%d (LPT), %d all-gather(s) of 72-B records, chain streamed on rank 0" % (world, chunks if sharded and not affine else 1)},
+                   "parallelism": "pair-sharded dp%d (LPT), %d all-gather(s) of 72-B records, chain streamed on rank 0%s" % (
+                       world, chunks if sharded and not affine else 1,
+                       "; one launch per rank, records streamed per pair (fused device finalize)" if stream else "")},
         "answer_hash_ok": answer_ok,
         "answer_source": expect["source"] if expect else None,
         "kernel": {"name": kernel, "fill_ms": round(fill_ms, 3), "traceback_ms": round(float(np.mean(traces)), 3),

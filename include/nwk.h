@@ -57,7 +57,9 @@ typedef struct nwk_opts {
   int32_t host_threads;      /* SHA-512 / finalize threads; 0 = min(16, cores) */
   int64_t workspace_bytes;   /* HBM budget per device; 0 = 92% of free memory */
   int32_t verbose;           /* 1 = per-call statistics on stderr */
-  int32_t finalize;          /* pair finalize (rows, penalty, SHA-512): 0 auto, 1 host, 2 device (nw_hash) */
+  int32_t finalize;          /* pair finalize (rows, penalty, SHA-512): 0 auto, 1 host, 2 device (nw_rows + nw_hash
+                                after each fill launch), 3 device fused into the nw_align_bits / nw_align_strip launch:
+                                each pair's record reaches the host as soon as it is hashed (nwk_align_pairs_poll) */
   int32_t linear_space;      /* linear-space traceback: 0 = only for pairs whose matrix exceeds
                                 the HBM budget, -1 = never, G > 0 = every pair, G bands per recompute group */
   int32_t kernel;            /* linear fill kernel: 0 auto (nw_align_bits where admissible: pxy >= 0, pgap 1 or 2,
@@ -68,7 +70,9 @@ typedef struct nwk_opts {
                                 exact -- W > 4, mixed-sign K, pgap > 2 -- falls back) */
   int32_t collective;        /* nwk_get_minimum_penalties: 1 = take the sharded RCCL all-gather path even when
                                 ngpus == 1 (one communicator of one rank; tests the collective on a 1-GPU box) */
-  int32_t reserved[1];
+  int32_t task_order;        /* nw_align_bits band tasks: 0 auto (band-major above one round of wave slots), 1 pair-major
+                                (pairs finish in the order given -- ascending ids stream out first, for
+                                nwk_align_pairs_poll), 2 band-major */
 } nwk_opts;
 
 typedef struct nwk_stats {
@@ -125,6 +129,17 @@ int nwk_align_pairs(nwk_ctx *ctx, const int64_t *pair_ids, int64_t npairs, int32
  */
 int nwk_align_pairs_begin(nwk_ctx *ctx, const int64_t *pair_ids, int64_t npairs, int32_t pxy, int32_t pgap);
 int nwk_align_pairs_end(nwk_ctx *ctx, int32_t *penalties, uint8_t *problem_hash);
+/*
+ * While a _begin call is in flight: copies the results of pair_ids[from ..
+ * *upto) -- the longest run from `from` whose results are final -- into
+ * penalties[] / problem_hash[] (indexed like pair_ids) and sets *upto.  With
+ * the bits kernels' fused device finalize, each pair's record streams to the
+ * host as soon as its traceback is done, so a rank can exchange (and rank 0
+ * chain) a prefix of its shard while the rest still aligns -- the reference
+ * collects results as they arrive, sub:305-331.  Returns the call's error once
+ * it has ended without every result.
+ */
+int nwk_align_pairs_poll(nwk_ctx *ctx, int64_t from, int32_t *penalties, uint8_t *problem_hash, int64_t *upto);
 
 /*
  * getMinimumPenalties on a context (skel:117-175, sub:232-364): aligns all

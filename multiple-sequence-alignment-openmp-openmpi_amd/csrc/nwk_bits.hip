@@ -40,6 +40,7 @@
 // steps within bits_w columns of the diagonal j = i n / m; a traceback that
 // leaves them flags the pair for a full-storage re-run (FillArgs::retry).
 #include "nwk_internal.h"
+#include "nwk_sha_dev.h"
 
 namespace nwk {
 namespace {
@@ -55,6 +56,15 @@ __device__ __forceinline__ unsigned long long bits_opaque_zero() {
   unsigned long long z = 0;
   asm volatile("" : "+v"(z));
   return z;
+}
+
+// Reads at the coherence point (an atomic add of 0): a plain load can hit a
+// stale line in this XCD's L2 when another XCD wrote the word during the launch
+__device__ __forceinline__ unsigned ld_fresh(const unsigned* p) {
+  return __hip_atomic_fetch_add((gu32*)p, (unsigned)bits_opaque_zero(), BITS_RLX);
+}
+__device__ __forceinline__ u64 ld_fresh64(const u64* p) {
+  return __hip_atomic_fetch_add((gu64*)p, bits_opaque_zero(), BITS_RLX);
 }
 
 // Polls the granules lanes 0..n-1 hold until every one carries `epoch`
@@ -329,7 +339,7 @@ constexpr int waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0F70; }
 #define NWK_TRACE_PRIO 0
 #endif
 __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd, unsigned char* obuf, int lane,
-                                           unsigned* prog) {
+                                           unsigned* prog, int& o_len, int2& o_end, bool& o_out) {
   const int nblk = pd.bits_nblk, win = pd.bits_w;
   const int64_t bdw = (int64_t)nblk * 1024;  // dwords per band
   // Storage map.  Banded tasks: band b's step s = c + r (its own numbering),
@@ -678,12 +688,241 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
   }
   flush(Lc);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // out of the window: a placeholder result (no moves) and the re-run flag;
+  // otherwise the walk ends on the border: row b * 2048 + r + 1, column c + 1
+  o_len = out ? 0 : Lc;
+  o_end = (a.dbg_notrace || out) ? make_int2(pd.m, pd.n) : make_int2(b * kBR + r + 1, c + 1);
+  o_out = out;
   if (lane == 0) {
-    // out of the window: a placeholder result (no moves) and the re-run flag
-    a.oplen[pd.slot] = out ? 0 : Lc;
-    // the walk ends on the border: row b * 2048 + r + 1, column c + 1
-    a.endij[pd.slot] = (a.dbg_notrace || out) ? make_int2(pd.m, pd.n) : make_int2(b * kBR + r + 1, c + 1);
+    a.oplen[pd.slot] = o_len;
+    a.endij[pd.slot] = o_end;
     if (out) a.retry[pd.slot] = 1;
+  }
+}
+
+// ---- Fused pair finalize (FillArgs::fuse_fin) ------------------------------
+// The same work as nw_rows + nw_hash (nwk_hash.hip), done inside the fill
+// launch so results leave the GPU as pairs finish.  The rows are built by the
+// wave that traced the pair (all 64 lanes busy); the SHA-512 -- sequential
+// within a row -- runs one row per lane on waves that claim 32 traced pairs at
+// a time from a queue, so every hashing instruction works for 64 rows (hashing
+// in the tracing wave itself, two lanes of 64, cost ~32x the issue and slowed
+// C3 by 3%, profiles/r03/ab/fused_finalize_not_kept.txt).
+
+// align1 / align2 (skel:263-272 prefix, then the moves in forward order: 64
+// per iteration, a wave scan of the packed x / y advances) and the path cost
+// (= dp[m][n], the reference's penalty) -> fin_len[slot], fin_len[np + slot]
+__device__ __forceinline__ void fin_rows(const FillArgs& a, const PairDesc& pd, int lane, int nops, int2 e) {
+  using namespace shadev;
+  const int pre = e.x > 0 ? e.x : e.y;
+  if (e.x < 0 || e.y < 0 || e.x > pd.m || e.y > pd.n || nops < 0 || pre + nops > pd.m + pd.n) {
+    if (lane == 0) atomicOr(a.err, 128u);  // (a walk that did not end on the border)
+    return;
+  }
+  const uint8_t* ops = a.ops + pd.ops_off;
+  const uint8_t* x = a.raw + pd.x_off;
+  const uint8_t* y = a.raw + pd.y_off;
+  uint8_t* r1 = a.rows1 + (pd.ops_off - a.ops_base);
+  uint8_t* r2 = a.rows2 + (pd.ops_off - a.ops_base);
+  for (int t = lane; t < pre; t += 64) {  // prefix run
+    r1[t] = e.x > 0 ? x[t] : (uint8_t)'_';
+    r2[t] = e.x > 0 ? (uint8_t)'_' : y[t];
+  }
+  int ix = e.x, iy = e.y;
+  int pen = 0;
+  for (int base = 0; base < nops; base += 64) {
+    const int f = base + lane;
+    const bool live = f < nops;
+    const unsigned op = live ? ops[nops - 1 - f] : 0u;
+    const bool d = op == 'D', up = op == 'U';
+    const bool ax = live && (d || up), ay = live && (d || !up);
+    const unsigned adv = (ax ? 1u : 0u) | (ay ? 0x10000u : 0u);
+    const unsigned inc = wave_incl_scan(adv, lane);
+    const unsigned exc = inc - adv;
+    if (live) {
+      const int xi = ix + (int)(exc & 0xffffu), yi = iy + (int)(exc >> 16);
+      if ((ax && xi >= pd.m) || (ay && yi >= pd.n)) {
+        atomicOr(a.err, 256u);  // (moves that leave the matrix)
+      } else {
+        const unsigned chx = ax ? x[xi] : (unsigned)'_';
+        const unsigned chy = ay ? y[yi] : (unsigned)'_';
+        r1[pre + f] = (uint8_t)chx;
+        r2[pre + f] = (uint8_t)chy;
+        pen += d ? (chx == chy ? 0 : a.pxy) : a.pgap;
+      }
+    }
+    const unsigned tot = (unsigned)__shfl((int)inc, 63);
+    ix += (int)(tot & 0xffffu);
+    iy += (int)(tot >> 16);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) pen += __shfl_xor(pen, o);
+  if (lane == 0) {
+    a.fin_len[pd.slot] = pre + nops;  // both rows have this length
+    a.fin_len[a.ntasks_pairs + pd.slot] = pen + pre * a.pgap;
+  }
+}
+
+// After fin_rows: publish the rows (a hashing wave may run on another XCD)
+// and queue the pair.  Every traced pair (also one that left its storage
+// window and re-runs later) is counted in hq_ctl[2].
+__device__ __forceinline__ void hq_push(const FillArgs& a, const PairDesc& pd, int lane, bool queue) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  if (lane == 0) {
+    if (queue) {
+      const unsigned pos = __hip_atomic_fetch_add(a.hq_ctl, 1u, BITS_RLX);
+      __hip_atomic_store((gu64*)(a.hq + pos), ((u64)a.epoch << 32) | (unsigned)pd.slot, BITS_RLX);
+    }
+    __hip_atomic_fetch_add(a.hq_ctl + 2, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Claims up to 32 queued pairs (at least 32 unless `drain`) and hashes them:
+// lane 2q + s runs SHA-512 over row s of pair q, the even lane then hashes the
+// two digests' hex (skel:155-157) and writes the host-mapped record and its
+// flag.  Returns whether it hashed anything.
+__device__ __forceinline__ bool hq_hash(const FillArgs& a, int lane, bool drain) {
+  using namespace shadev;
+  unsigned tail = 0, head = 0;
+  if (lane == 0) {
+    tail = ld_fresh(a.hq_ctl);
+    head = ld_fresh(a.hq_ctl + 1);
+  }
+  tail = __builtin_amdgcn_readfirstlane(tail);
+  head = __builtin_amdgcn_readfirstlane(head);
+  const unsigned avail = tail - head;
+  if (avail == 0 || avail > 0x7fffffffu || (!drain && avail < 32)) return false;
+  const unsigned want = avail < 32 ? avail : 32;
+  unsigned ok = 0;
+  if (lane == 0)
+    ok = __hip_atomic_compare_exchange_strong(a.hq_ctl + 1, &head, head + want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
+  if (!__builtin_amdgcn_readfirstlane(ok)) return false;  // another wave took them: the caller retries
+  head = __builtin_amdgcn_readfirstlane(head);
+  const int q = lane >> 1, side = lane & 1;
+  const bool live = q < (int)want;
+  u64 ent = 0;
+  if (live) {  // the producer reserved the entry just before writing it
+    const u64 t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      ent = ld_fresh64(a.hq + head + q);
+      if ((unsigned)(ent >> 32) == a.epoch) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) break;
+    }
+  }
+  const bool ok_ent = !live || (unsigned)(ent >> 32) == a.epoch;
+  if (!__all(ok_ent)) {
+    if (lane == 0) atomicOr(a.err, 32u);
+    return true;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the producers' rows
+  const int slot = live ? (int)(unsigned)ent : 0;
+  // (row length and penalty were written on the producer's XCD: fresh reads)
+  int64_t L = live ? (int)ld_fresh(reinterpret_cast<const unsigned*>(a.fin_len + slot)) : 0;
+  // (a queue entry or row length outside its pair: report, hash nothing)
+  const bool sane = !live || ((unsigned)slot < (unsigned)a.ntasks_pairs && L >= 0 &&
+                              L <= (int64_t)a.pairs[slot].m + a.pairs[slot].n);
+  if (!__all(sane)) {
+    if (lane == 0) atomicOr(a.err, 64u);
+    return true;
+  }
+  const uint4* row = reinterpret_cast<const uint4*>((side ? a.rows2 : a.rows1) + (a.pairs[slot].ops_off - a.ops_base));
+  Sha sh;
+  sh.init();
+  const int64_t nblk = live ? (L + 17 + 127) / 128 : 0, ndata = (L + 127) / 128;
+  int64_t wblk = nblk;  // per wave: as many blocks as its longest row
+  for (int o = 32; o > 0; o >>= 1) wblk = max(wblk, (int64_t)__shfl_xor(wblk, o));
+  uint4 cur[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) cur[k] = ndata > 0 ? row[k] : make_uint4(0, 0, 0, 0);
+  for (int64_t bk = 0; bk < wblk; ++bk) {
+    uint64_t w[16];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // little-endian dwords -> big-endian 64-bit words
+      w[2 * k] = ((uint64_t)__builtin_bswap32(cur[k].x) << 32) | __builtin_bswap32(cur[k].y);
+      w[2 * k + 1] = ((uint64_t)__builtin_bswap32(cur[k].z) << 32) | __builtin_bswap32(cur[k].w);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cur[k] = bk + 1 < ndata ? row[8 * (bk + 1) + k] : make_uint4(0, 0, 0, 0);
+    const int64_t b0 = 128 * bk;  // message bytes [b0, b0 + 128)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {  // clear bytes past L, place the 0x80 terminator
+      const int64_t s0 = b0 + 8 * k;
+      if (s0 + 8 > L) {
+        const int keep = (int)max((int64_t)0, min((int64_t)8, L - s0));
+        uint64_t v = keep > 0 ? w[k] & (~0ull << (64 - 8 * keep)) : 0ull;
+        if (L >= s0 && L < s0 + 8) v |= 0x80ull << (56 - 8 * (L - s0));
+        w[k] = v;
+      }
+    }
+    if (bk == nblk - 1) w[15] = (uint64_t)L * 8u;
+    if (bk < nblk) sh.block_rolled(w);
+  }
+  uint64_t other[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) other[k] = __shfl_xor(sh.s[k], 1);
+  if (live && side == 0) {
+    Sha p;
+    p.init();
+    uint64_t w[16];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      w[2 * k] = hex16((uint32_t)(sh.s[k] >> 32));
+      w[2 * k + 1] = hex16((uint32_t)sh.s[k]);
+    }
+    p.block_rolled(w);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      w[2 * k] = hex16((uint32_t)(other[k] >> 32));
+      w[2 * k + 1] = hex16((uint32_t)other[k]);
+    }
+    p.block_rolled(w);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = 0;
+    w[0] = 0x8000000000000000ULL;
+    w[15] = 256 * 8;
+    p.block_rolled(w);
+    uint64_t* out = reinterpret_cast<uint64_t*>(a.fin_hash + 64 * (int64_t)slot);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[k] = __builtin_bswap64(p.s[k]);
+    a.fin_pen[slot] = (int)ld_fresh(reinterpret_cast<const unsigned*>(a.fin_len + a.ntasks_pairs + slot));
+    __threadfence_system();  // the record, then its flag (the host polls it during the launch)
+    __hip_atomic_store(a.fin_flag + slot, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  return true;
+}
+
+// Out of fill tasks: at most kDrainWaves waves stay to hash what is left
+// until every pair of the launch is traced and claimed (bounded like the
+// hand-off waits: ~4 s without progress, or another wave's failure).
+constexpr unsigned kDrainWaves = 64;
+__device__ __forceinline__ void hq_drain(const FillArgs& a, int lane) {
+  unsigned w = 0;
+  if (lane == 0) w = __hip_atomic_fetch_add(a.hq_ctl + 3, 1u, BITS_RLX);
+  if (__builtin_amdgcn_readfirstlane(w) >= kDrainWaves) return;
+  u64 t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (hq_hash(a, lane, true)) {
+      t0 = __builtin_amdgcn_s_memrealtime();
+      continue;
+    }
+    unsigned traced = 0, tail = 0, head = 0;
+    if (lane == 0) {
+      traced = ld_fresh(a.hq_ctl + 2);
+      tail = ld_fresh(a.hq_ctl);
+      head = ld_fresh(a.hq_ctl + 1);
+    }
+    traced = __builtin_amdgcn_readfirstlane(traced);
+    tail = __builtin_amdgcn_readfirstlane(tail);
+    head = __builtin_amdgcn_readfirstlane(head);
+    if (traced >= (unsigned)a.ntasks_pairs && head == tail) return;
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)a.err, BITS_RLX)) != 0u) return;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
+      if (lane == 0) atomicOr(a.err, 32u);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(32);
   }
 }
 
@@ -713,11 +952,19 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
   if (a.stamps && threadIdx.x == 0) atomicMin(a.stamps + 11 * a.ntasks_pairs, (u64)__builtin_amdgcn_s_memrealtime());
 
   for (;;) {
+    if (a.fuse_fin) {  // queued pairs to hash: whole groups between fill tasks
+      while (hq_hash(a, lane, false)) {
+      }
+    }
     unsigned tk = 0;
     if (lane == 0) tk = atomicAdd(a.counter, 1u);
     tk = __builtin_amdgcn_readfirstlane(tk);
     BITS_PROG(0x10000000u | tk);
-    if (tk >= (unsigned)a.ntasks) { BITS_PROG(0x60000000u); return; }
+    if (tk >= (unsigned)a.ntasks) {
+      if (a.fuse_fin) hq_drain(a, lane);
+      BITS_PROG(0x60000000u);
+      return;
+    }
     // wave-uniform exit (a per-lane load would make the task loop divergent)
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)a.err, BITS_RLX)) != 0u) return;
     const int2 task = a.tasks[tk];
@@ -867,10 +1114,17 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
       // the walk is one latency-bound wave: let it issue ahead of the SIMD's fill waves
       __builtin_amdgcn_s_setprio(3);
 #endif
-      trace_bits(a, pd, obuf_all[wid], lane, prog);
+      int tlen;
+      int2 tend;
+      bool tout;
+      trace_bits(a, pd, obuf_all[wid], lane, prog, tlen, tend, tout);
 #if NWK_TRACE_PRIO
       __builtin_amdgcn_s_setprio(0);
 #endif
+      if (a.fuse_fin) {
+        if (!tout) fin_rows(a, pd, lane, tlen, tend);
+        hq_push(a, pd, lane, !tout);
+      }
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
       BITS_PROG(0x56000000u);
     }
@@ -919,11 +1173,19 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
   constexpr int NG = 2 * NP;  // packed dwords per 64-column chunk of a pass's last row
 
   for (;;) {
+    if (a.fuse_fin) {
+      while (hq_hash(a, lane, false)) {
+      }
+    }
     unsigned tk = 0;
     if (lane == 0) tk = atomicAdd(a.counter, 1u);
     tk = __builtin_amdgcn_readfirstlane(tk);
     BITS_PROG(0x10000000u | tk);
-    if (tk >= (unsigned)a.ntasks) { BITS_PROG(0x60000000u); return; }
+    if (tk >= (unsigned)a.ntasks) {
+      if (a.fuse_fin) hq_drain(a, lane);
+      BITS_PROG(0x60000000u);
+      return;
+    }
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)a.err, BITS_RLX)) != 0u) return;
     const PairDesc pd = a.pairs[a.tasks[tk].x];
     const int np = pd.bits_np, nch = np >> 6, nb = pd.nbands, nsb = pd.sblocks;
@@ -1060,7 +1322,14 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
     BITS_PROG(0x40000000u);
-    trace_bits(a, pd, obuf_all[wid], lane, prog);
+    int tlen;
+    int2 tend;
+    bool tout;
+    trace_bits(a, pd, obuf_all[wid], lane, prog, tlen, tend, tout);
+    if (a.fuse_fin) {
+      if (!tout) fin_rows(a, pd, lane, tlen, tend);
+      hq_push(a, pd, lane, !tout);
+    }
     if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
     BITS_PROG(0x56000000u);
   }

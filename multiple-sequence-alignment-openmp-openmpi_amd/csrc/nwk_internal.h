@@ -136,6 +136,24 @@ struct FillArgs {
   const unsigned* yw;      // kBits: per y position p two dwords (code bit planes of y[p .. p+31], y[p] at bit 31), at pairs[].e_off
   int* retry;              // windowed storage: per slot, 1 = the path left the stored window (re-run in full)
   int strip_ring;          // kBitsStrip: LDS dwords per wave of the hand-off ring (max n' / 64 x 2 NP)
+  // Fused pair finalize (kBits / kBitsStrip with device finalize, nwk_bits.hip):
+  // the wave that traced a pair writes its rows and penalty (whole wave) and
+  // queues the pair; a wave that finds >= 32 queued pairs (or, once the fill
+  // tasks are gone, any) hashes them one row per lane, as nw_hash does, and
+  // writes the records {penalty, problemhash} and then fin_flag[slot] = epoch
+  // into host-mapped memory, so the host takes results during the launch.
+  int fuse_fin;
+  int pxy, pgap;           // linear move costs (penalty sum)
+  const uint8_t* raw;      // raw sequence bytes (codes layout)
+  int64_t ops_base;        // rows sit at rows1/2 + (ops_off - ops_base)
+  uint8_t* rows1;
+  uint8_t* rows2;
+  int* fin_len;            // per slot (device): row length, then the penalty at [np + slot]
+  unsigned long long* hq;  // queue of traced pairs: {epoch:32 | slot:32}, np entries
+  unsigned* hq_ctl;        // [0] entries reserved, [1] entries claimed, [2] pairs traced, [3] drain waves
+  int* fin_pen;            // per slot (host-mapped)
+  uint8_t* fin_hash;       // per slot, 64 raw bytes (host-mapped)
+  unsigned* fin_flag;      // per slot (host-mapped): = epoch once the record is written
 };
 constexpr int kProfSyms = 6;  // kProfileDP: symbols + gap per column profile
 

@@ -106,12 +106,12 @@ struct DevBuf {
 struct HostBuf {
   void* p = nullptr;
   size_t cap = 0;
-  int ensure(size_t bytes) {
+  int ensure(size_t bytes, unsigned flags = hipHostMallocDefault) {
     if (bytes <= cap) return NWK_OK;
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
-    HIP_TRY(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&p, bytes, flags));
     cap = bytes;
     return NWK_OK;
   }
@@ -172,12 +172,19 @@ struct nwk_ctx {
   DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij, d_done, d_stamps, d_prog, d_retry;
   DevBuf d_segctl;              // kPacked2: task-done flags | segment info | traceback records
   DevBuf d_pen, d_hash;         // device finalize (nw_hash): per pair penalty, problemhash
+  DevBuf d_hq;                  // fused finalize: queue of traced pairs | row lengths and penalties
   DevBuf d_msa[3];              // nwk_msa: row profiles | column profiles | granules, matrices, moves
   HostBuf h_pen[2], h_hash[2];
   bool has_us = false;          // some input byte is '_': trims need the host finalize
   HostBuf h_tasks;
   HostBuf h_pairs[2], h_oplen[2], h_endij[2], h_ops[2];  // double-buffered: batch b+1 runs while b finalizes
   HostBuf h_retry;  // kBits windowed storage: per slot of the last batch, 1 = re-run with full storage
+  // fused finalize (bits kernels): host-mapped coherent records the kernel
+  // writes per pair as it is traced, {flag u32 [np] | penalty i32 [np] | hash [np][64]}
+  HostBuf h_rec[2];
+  // set while an nwk_align_pairs_begin call runs: align_work marks each
+  // caller index whose final result is in place (nwk_align_pairs_poll)
+  std::atomic<uint8_t>* ready_out = nullptr;
 
   nwk_stats stats{};
 
@@ -187,6 +194,8 @@ struct nwk_ctx {
   std::vector<int64_t> a_ids;
   std::vector<int32_t> a_pen;
   std::vector<uint8_t> a_hash;
+  std::unique_ptr<std::atomic<uint8_t>[]> a_ready;
+  std::atomic<int> a_finished{0};  // the in-flight call has returned (a_rc is final)
   int a_rc = NWK_OK;
   std::string a_err;
 };
@@ -219,9 +228,9 @@ void nwk_ctx_destroy(nwk_ctx* c) {
   c->d_pairs.release(); c->d_tasks.release(); c->d_ctl.release();
   c->d_oplen.release(); c->d_endij.release(); c->d_done.release(); c->d_stamps.release(); c->d_retry.release();
   c->h_retry.release();
-  c->d_segctl.release(); c->d_prog.release(); c->d_pen.release(); c->d_hash.release();
+  c->d_segctl.release(); c->d_prog.release(); c->d_pen.release(); c->d_hash.release(); c->d_hq.release();
   for (auto& b : c->d_msa) b.release();
-  for (int b = 0; b < 2; ++b) { c->h_pen[b].release(); c->h_hash[b].release(); }
+  for (int b = 0; b < 2; ++b) { c->h_pen[b].release(); c->h_hash[b].release(); c->h_rec[b].release(); }
   c->h_tasks.release();
   for (int b = 0; b < 2; ++b) {
     c->h_pairs[b].release(); c->h_oplen[b].release(); c->h_endij[b].release(); c->h_ops[b].release();
@@ -240,8 +249,9 @@ int nwk_ctx_create(const nwk_opts* opts, nwk_ctx** out) {
   if (opts) o = *opts;
   if (const char* v = getenv("NWK_VERBOSE")) o.verbose = atoi(v);  // debug: diagnostics on stderr
   // option checks first: they need no device
-  if (o.finalize < 0 || o.finalize > 2) return fail(NWK_EINVAL, "nwk_ctx_create: finalize must be 0/1/2");
+  if (o.finalize < 0 || o.finalize > 3) return fail(NWK_EINVAL, "nwk_ctx_create: finalize must be 0..3");
   if (o.kernel < 0 || o.kernel > 5) return fail(NWK_EINVAL, "nwk_ctx_create: kernel must be 0..5");
+  if (o.task_order < 0 || o.task_order > 2) return fail(NWK_EINVAL, "nwk_ctx_create: task_order must be 0..2");
   if (o.bits != 0 && o.bits != 4 && o.bits != 8 && o.bits != 16 && o.bits != 32)
     return fail(NWK_EINVAL, "nwk_ctx_create: bits must be 0/4/8/16/32");
   if (ndev <= 0) return fail(NWK_EDEVICE, "nwk_ctx_create: no HIP device visible");
@@ -601,7 +611,10 @@ void footprint(PairWork* w, int bits, int mode, bool affine) {
     w->spec = 0;
     strip_storage(w);
     w->bnd_gr = 0;  // the pass-to-pass hand-off stays in LDS
-    w->ops_b = round_up((int64_t)w->m + w->n, 16);
+    // whole 128-byte lines per pair: the fused finalize's rows (op-region
+    // layout) are written on one XCD and hashed on another, so no line may be
+    // shared with a neighbour's rows (a stale copy in the hashing XCD's L2)
+    w->ops_b = round_up((int64_t)w->m + w->n, 128);
     return;
   }
   if (mode == kBits) {
@@ -611,7 +624,7 @@ void footprint(PairWork* w, int bits, int mode, bool affine) {
     w->bits_nblk = (int)bits_nblk_of(w->m, w->n, w->bits_w);
     w->mat_dw = nb * w->bits_nblk * 1024;
     w->bnd_gr = (nb - 1) * nch * kBitsGranPerChunk;
-    w->ops_b = round_up((int64_t)w->m + w->n, 16);
+    w->ops_b = round_up((int64_t)w->m + w->n, 128);  // (whole lines per pair, as above)
     return;
   }
   const int64_t nb = ceil_div(w->m, kBandRows);
@@ -713,6 +726,20 @@ void parallel_for(int threads, int64_t n, F&& f) {
 // The answer-hash chain of skel:159 advanced while later batches still run:
 // results are marked ready by output index (= canonical pair id for a full
 // call) and the chain consumes the ready prefix.
+// caller index q's final result is in place (nwk_align_pairs_poll)
+inline void mark_ready(nwk_ctx* c, int64_t q) {
+  if (c->ready_out) c->ready_out[q].store(1, std::memory_order_release);
+}
+
+// Fused finalize: the host side of one batch's streamed records (see the
+// consumer in align_work).  done: 0 running, 1 kernel finished (skip holds
+// the window re-runs), 2 abandoned (an error path left align_work).
+struct FusedSync {
+  std::atomic<int> done{0};
+  std::vector<char> skip;
+  int64_t missing = 0;
+};
+
 struct Chain {
   const uint8_t* hashes = nullptr;  // [P][64] raw problem hashes
   std::vector<char> ready;
@@ -1046,6 +1073,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       penalties[w.out] = f.penalty;
       memcpy(hashes + 64 * w.out, f.hash, 64);
       if (chain) chain->ready[w.out] = 1;
+      mark_ready(c, w.out);
     } else {
       footprint(&w, pl.bits, pl.mode, sc.affine);
       dp.push_back(w);
@@ -1167,10 +1195,11 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   // est. device ms ~ 0.007 per 128-byte block of the longest row (per wave
   // slot round), host ~ 350 bytes/us per thread.  NWK_DEVHASH=0/1 forces.
   static const int devhash_env = getenv("NWK_DEVHASH") ? atoi(getenv("NWK_DEVHASH")) : -1;
-  const int fin_mode = c->opts.finalize == 1 ? 0 : c->opts.finalize == 2 ? 1 : devhash_env;
+  const int fin_mode = c->opts.finalize == 1 ? 0 : c->opts.finalize >= 2 ? 1 : devhash_env;
   const bool dev_ok = a1 == nullptr && !c->has_us && fin_mode != 0;
   if (dev_ok && !dp.empty() && (rc = build_encoding(c, 1)) != NWK_OK) return rc;
   size_t pos = 0;
+  std::vector<std::shared_ptr<FusedSync>> fused_all;  // streamed batches (checked after the last join)
   double h_setup = 0, h_sync = 0, h_join = 0, h_last = 0;  // host phases (verbose)
   const bool lin_all = c->opts.linear_space > 0 && !sc.affine;  // (tests: every pair through f2)
   while (pos < dp.size()) {
@@ -1217,6 +1246,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         penalties[w.out] = fs[q].penalty;
         memcpy(hashes + 64 * w.out, fs[q].hash, 64);
         if (chain) chain->ready[w.out] = 1;
+        mark_ready(c, w.out);
       }
       if (chain) chain->advance();
       pos = lend;
@@ -1315,6 +1345,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     int64_t t = 0;
     static const int order_env = getenv("NWK_ORDER") ? atoi(getenv("NWK_ORDER")) : -1;
     int order = order_env;
+    if (order < 0 && pl.mode == kBits && c->opts.task_order > 0) order = c->opts.task_order == 1 ? 0 : 1;
     if (order < 0) order = (pl.mode == kBits || pl.mode == kAffinePk) && ntasks > 4 * (int64_t)grid ? 1 : 0;
     if (pl.mode == kBitsStrip) order = 0;  // one task per pair, largest first
     if (order == 1) {  // band-major (experiment)
@@ -1416,6 +1447,45 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.segops = c->d_work.as<uint8_t>() + segops_base_b;
     fa.oplen = c->d_oplen.as<int>();
     fa.endij = c->d_endij.as<int2>();
+    // finalize 3: the bits kernels' device finalize fused into the fill launch
+    // (rows by the tracing wave, SHA-512 by waves that claim 32 traced pairs
+    // from a queue: nwk_bits.hip fin_rows / hq_hash), records streaming to the
+    // host while it runs.  Only on request: on one GPU the separate nw_rows +
+    // nw_hash is faster (C3 161.5 vs 165.4 ms per step, C4 100.9 vs 106.1),
+    // but a rank of a sharded job can exchange and chain finished pairs early.
+    const bool fuse = devhash && c->opts.finalize == 3 && bitsy && !fa.dbg_notrace && !sc.affine;
+    if (devhash) {
+      if ((rc = c->d_pen.ensure(4 * (size_t)np)) != NWK_OK) return rc;
+      if ((rc = c->d_hash.ensure(64 * (size_t)np)) != NWK_OK) return rc;
+    }
+    unsigned* rflag = nullptr;
+    int* rpen = nullptr;
+    uint8_t* rhash = nullptr;
+    if (fuse) {
+      const size_t rb = (size_t)np * 72;
+      if ((rc = c->h_rec[par].ensure(rb, hipHostMallocMapped | hipHostMallocCoherent)) != NWK_OK) return rc;
+      rflag = c->h_rec[par].as<unsigned>();
+      rpen = reinterpret_cast<int*>(rflag + np);
+      rhash = reinterpret_cast<uint8_t*>(rpen + np);
+    }
+    if (fuse) {
+      fa.fuse_fin = 1;
+      fa.pxy = sc.pxy;
+      fa.pgap = sc.pgap;
+      fa.raw = c->d_codes[1].as<uint8_t>();
+      fa.ops_base = ops_base_b;
+      fa.rows1 = c->d_work.as<uint8_t>() + rows_base_b;
+      fa.rows2 = fa.rows1 + ops + 256;
+      void *dflag = nullptr;
+      HIP_TRY(hipHostGetDevicePointer(&dflag, rflag, 0));
+      fa.fin_flag = static_cast<unsigned*>(dflag);
+      fa.fin_pen = reinterpret_cast<int*>(fa.fin_flag + np);
+      fa.fin_hash = reinterpret_cast<uint8_t*>(fa.fin_pen + np);
+      if ((rc = c->d_hq.ensure((8 + 8) * (size_t)np)) != NWK_OK) return rc;  // queue | row lengths, penalties
+      fa.hq = c->d_hq.as<unsigned long long>();
+      fa.fin_len = reinterpret_cast<int*>(fa.hq + np);
+      fa.hq_ctl = c->d_ctl.as<unsigned>() + 32;  // (d_ctl's 256 bytes are zeroed per batch)
+    }
     // One persistent launch: fill bands, and each pair's traceback runs on
     // the wave that finishes the pair's last band (nw_align).
     if (c->opts.verbose >= 3) {
@@ -1433,9 +1503,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       HIP_TRY(launch_fill(pl.mode, pl.bits, fa, std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     if (seg) HIP_TRY(launch_gather(fa, np, pl.mode == kPacked2 ? 1 : 0, c->stream));  // segment chains -> op strings
-    if (devhash) {
-      if ((rc = c->d_pen.ensure(4 * (size_t)np)) != NWK_OK) return rc;
-      if ((rc = c->d_hash.ensure(64 * (size_t)np)) != NWK_OK) return rc;
+    if (devhash && !fuse) {
       HashArgs ha;
       ha.pairs = fa.pairs;
       ha.npairs = np;
@@ -1454,6 +1522,58 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       HIP_TRY(launch_hash(ha, c->stream));
     }
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    // Fused finalize: a host thread takes each pair's record as its flag
+    // arrives (host-mapped, written by the wave that traced the pair) and
+    // feeds the chain while the launch still runs.
+    std::shared_ptr<FusedSync> fsync;
+    struct FuseGuard {  // an early return abandons the consumer instead of leaving it waiting
+      std::shared_ptr<FusedSync>* f;
+      ~FuseGuard() {
+        int z = 0;
+        if (*f) (*f)->done.compare_exchange_strong(z, 2);
+      }
+    } fguard{&fsync};
+    if (fuse) {
+      fin.join();
+      fsync = std::make_shared<FusedSync>();
+      const PairWork* dwf = dp.data() + pos;  // (dp never reallocates: reserved for every re-run)
+      const unsigned ep = fa.epoch;
+      fin.start([c, np, dwf, fsync, ep, rflag, rpen, rhash, penalties, hashes, chain]() {
+        std::vector<char> got((size_t)np, 0);
+        int64_t lo = 0, ngot = 0;
+        for (;;) {
+          const int d = fsync->done.load(std::memory_order_acquire);
+          if (d == 2) return;
+          bool any = false;
+          const int64_t hi = d ? np : std::min<int64_t>(np, lo + 8192);
+          for (int64_t q = lo; q < hi; ++q) {
+            if (got[(size_t)q] || __atomic_load_n(rflag + q, __ATOMIC_ACQUIRE) != ep) continue;
+            const PairWork& w = dwf[q];
+            penalties[w.out] = rpen[q];
+            memcpy(hashes + 64 * w.out, rhash + 64 * q, 64);
+            if (chain) {
+              chain->prepare(w.out);
+              chain->ready[w.out] = 1;
+            }
+            mark_ready(c, w.out);
+            got[(size_t)q] = 1;
+            ++ngot;
+            any = true;
+          }
+          while (lo < np && got[(size_t)lo]) ++lo;
+          if (chain && any) chain->advance();
+          if (d || ngot == np) break;
+          if (!any) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+        // every pair without a record must be a window re-run
+        if (ngot < np) {
+          while (fsync->done.load(std::memory_order_acquire) == 0) std::this_thread::sleep_for(std::chrono::microseconds(20));
+          if (fsync->done.load() == 2) return;
+          for (int64_t q = 0; q < np; ++q)
+            if (!got[(size_t)q] && !(!fsync->skip.empty() && fsync->skip[(size_t)q])) ++fsync->missing;
+        }
+      });
+    }
     if (c->opts.verbose >= 3) {
       fprintf(stderr, "nwk batch %d: launched mode %d bits %d grid %d, waiting\n", st.batches, pl.mode, pl.bits, grid);
       fflush(stderr);
@@ -1480,7 +1600,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipMemcpyAsync(c->h_oplen[par].p, fa.oplen, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_endij[par].p, fa.endij, sizeof(int2) * np, hipMemcpyDeviceToHost, c->stream));
     if (windowed) HIP_TRY(hipMemcpyAsync(c->h_retry.p, fa.retry, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
-    if (devhash) {  // 68 bytes per pair instead of the move strings
+    if (fuse) {
+      // records arrive in host memory on their own
+    } else if (devhash) {  // 68 bytes per pair instead of the move strings
       if ((rc = c->h_pen[par].ensure(4 * (size_t)np)) != NWK_OK) return rc;
       if ((rc = c->h_hash[par].ensure(64 * (size_t)np)) != NWK_OK) return rc;
       HIP_TRY(hipMemcpyAsync(c->h_pen[par].p, c->d_pen.p, 4 * (size_t)np, hipMemcpyDeviceToHost, c->stream));
@@ -1623,6 +1745,20 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         st.window_retries += 1;
       }
     }
+    if (fuse) {  // the consumer finishes on its own; the next join collects it
+      fsync->skip = skip;
+      fsync->done.store(1, std::memory_order_release);
+      h_setup += tb1 - tb0;
+      h_sync += tb2 - tb1;
+      fused_all.push_back(fsync);
+      if (end >= dp.size()) {
+        const double tf0 = now_ms();
+        fin.join();
+        h_last += now_ms() - tf0;
+      }
+      pos = end;
+      continue;
+    }
     // ---- host finalize, overlapped with the next batch's kernel: it runs on
     // its own thread over this batch's host buffer set while the loop goes
     // on to set up, launch and wait for batch b+1 (buffer set par ^ 1).
@@ -1654,6 +1790,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         penalties[w.out] = f.penalty;
         memcpy(hashes + 64 * w.out, f.hash, 64);
       });
+      for (int64_t q = 0; q < np; ++q)
+        if (!skipped(q)) mark_ready(c, dw[q].out);
       if (chain) {  // serial: jobs never overlap each other (fin.join() before the next starts)
         parallel_for(c->host_threads, (np + 255) / 256, [&](int64_t b) {  // second-block schedules, in parallel
           for (int64_t q = b * 256; q < std::min<int64_t>(np, (b + 1) * 256); ++q)
@@ -1671,6 +1809,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     pos = end;
   }
   fin.join();
+  for (const auto& f : fused_all)
+    if (f->missing) return fail(NWK_EKERNEL, "fused finalize: %lld pair(s) without a record", (long long)f->missing);
   st.total_ms = now_ms() - t_start;
   if (c->opts.verbose)
     fprintf(stderr, "nwk host: setup+launch %.3f ms, kernel+copies wait %.3f ms, finalize join %.3f ms, last finalize %.3f ms\n", h_setup, h_sync, h_join, h_last);
@@ -1727,11 +1867,35 @@ int nwk_align_pairs_begin(nwk_ctx* c, const int64_t* pair_ids, int64_t npairs, i
   c->pending = true;
   c->a_rc = NWK_OK;
   c->a_err.clear();
+  c->a_ready.reset(new std::atomic<uint8_t>[(size_t)std::max<int64_t>(npairs, 1)]);
+  for (int64_t q = 0; q < std::max<int64_t>(npairs, 1); ++q) c->a_ready[q].store(0, std::memory_order_relaxed);
+  c->a_finished.store(0);
   c->async = std::thread([c, pxy, pgap]() {
+    c->ready_out = c->a_ready.get();
     c->a_rc = nwk_align_pairs(c, c->a_ids.data(), (int64_t)c->a_ids.size(), pxy, pgap, c->a_pen.data(),
                               c->a_hash.data());
+    c->ready_out = nullptr;
     if (c->a_rc != NWK_OK) c->a_err = g_err;
+    c->a_finished.store(1, std::memory_order_release);
   });
+  return NWK_OK;
+}
+
+int nwk_align_pairs_poll(nwk_ctx* c, int64_t from, int32_t* penalties, uint8_t* problem_hash, int64_t* upto) {
+  if (!c || !c->pending || !upto || from < 0) return fail(NWK_EINVAL, "nwk_align_pairs_poll: bad argument");
+  const int64_t n = (int64_t)c->a_ids.size();
+  if (from > n) return fail(NWK_EINVAL, "nwk_align_pairs_poll: from %lld > %lld pairs", (long long)from, (long long)n);
+  if (from < n && (!penalties || !problem_hash)) return fail(NWK_EINVAL, "nwk_align_pairs_poll: bad argument");
+  const bool finished = c->a_finished.load(std::memory_order_acquire) != 0;
+  int64_t q = from;
+  while (q < n && c->a_ready[q].load(std::memory_order_acquire)) ++q;
+  if (q > from) {
+    memcpy(penalties + from, c->a_pen.data() + from, 4 * (size_t)(q - from));
+    memcpy(problem_hash + 64 * from, c->a_hash.data() + 64 * from, 64 * (size_t)(q - from));
+  }
+  *upto = q;
+  // a call that ended without every result: its error (nwk_align_pairs_end reports it too)
+  if (finished && q < n && c->a_rc != NWK_OK) return fail(c->a_rc, "%s", c->a_err.c_str());
   return NWK_OK;
 }
 

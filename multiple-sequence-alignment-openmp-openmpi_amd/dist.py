@@ -181,6 +181,89 @@ def align_sharded_pipelined(eng, lengths, pxy, pgap, rank, world, chunks=1, devi
             chain.close()
 
 
+def align_sharded_streamed(eng, lengths, pxy, pgap, rank, world, chunks=8, device=None, group=None,
+                           on_piece=None, poll_s=50e-6):
+    """The shard as ONE launch (Engine.align_pairs_begin over its ids in
+    ascending canonical order, the engine built with finalize="fused") whose
+    per-pair records stream to the host as pairs are hashed inside the fill
+    launch (Engine.align_pairs_poll).
+    Piece c -- the shard's ids below the global threshold P (c+1) / chunks --
+    goes through its all-gather as soon as all of its records are in, and rank
+    0's chain worker advances over it while the rest of the shard still
+    aligns: sub:305-331 collects results as they arrive, sub:334-337 chains.
+    Same return value and failure contract as align_sharded_pipelined."""
+    import time
+
+    k = len(lengths)
+    P = k * (k - 1) // 2
+    parts, per = chunk_parts(lengths, rank, world, chunks)
+    ids = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int64)
+    bounds = np.cumsum([0] + [len(x) for x in parts])
+    chain = seqalign.ChainStream(P) if rank == 0 else None
+    pen = np.zeros(max(len(ids), 1), dtype=np.int32)
+    hs = np.zeros((max(len(ids), 1), 64), dtype=np.uint8)
+    err = None
+    pending = False
+    got = 0
+    try:
+        try:
+            eng.align_pairs_begin(ids, pxy, pgap)
+            pending = True
+        except Exception as e:
+            err = e
+        for c in range(chunks):
+            rec = None
+            if err is None:
+                try:
+                    while got < bounds[c + 1]:
+                        u, p_, h_ = eng.align_pairs_poll(got)
+                        if u > got:
+                            pen[got:u] = p_
+                            hs[got:u] = h_
+                            got = u
+                        elif got < bounds[c + 1]:
+                            time.sleep(poll_s)
+                    if on_piece is not None:
+                        on_piece(c)
+                    lo, hi = bounds[c], bounds[c + 1]
+                    rec = pack_records(parts[c], pen[lo:hi], hs[lo:hi], per[c])
+                except Exception as e:
+                    err = e
+            if rec is None:  # still join the collective, so no peer waits forever
+                rec = pack_records([], [], [], per[c])
+                rec[:, :4] = np.array([FAILED], dtype=np.int32).view(np.uint8)
+            g = all_gather_records(rec, device=device, group=group)
+            if err is not None:
+                continue
+            try:
+                cid, cpen, chs = unpack_chunk(g)
+            except RankFailed as e:  # every rank sees it in the same gather
+                err = e
+                continue
+            if chain is not None:
+                chain.feed(cid, cpen, chs)
+        if pending:
+            pending = False
+            try:
+                eng.align_pairs_end()
+            except Exception as e:
+                if err is None:
+                    err = e
+        if err is not None:
+            raise RankFailed("rank %d: %s" % (rank, err)) from err
+        if chain is None:
+            return None, None, None
+        return chain.finish()
+    finally:
+        if pending:
+            try:
+                eng.align_pairs_end()
+            except Exception:
+                pass
+        if chain is not None:
+            chain.close()
+
+
 def align_sharded(align_fn, lengths, pxy, pgap, rank, world, device=None, group=None):
     """Runs this rank's shard through align_fn(ids, pxy, pgap) -> (pen, hashes),
     gathers every rank's records and returns (penalties[P], hashes[P,64], ids)."""

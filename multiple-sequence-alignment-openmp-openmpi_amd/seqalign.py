@@ -41,7 +41,7 @@ class Opts(ctypes.Structure):
                 ("host_threads", ctypes.c_int32), ("workspace_bytes", ctypes.c_int64),
                 ("verbose", ctypes.c_int32), ("finalize", ctypes.c_int32),
                 ("linear_space", ctypes.c_int32), ("kernel", ctypes.c_int32), ("collective", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 1)]
+                ("task_order", ctypes.c_int32)]
 
 
 class Stats(ctypes.Structure):
@@ -80,6 +80,7 @@ SIGNATURES = {
     "nwk_sha512_hex": (None, [_P, _I64, _P]),
     "nwk_align_pairs_begin": (ctypes.c_int, [_P, _P, _I64, _I32, _I32]),
     "nwk_align_pairs_end": (ctypes.c_int, [_P, _P, _P]),
+    "nwk_align_pairs_poll": (ctypes.c_int, [_P, _I64, _P, _P, _P]),
     "nwk_chain_create": (ctypes.c_int, [_I64, _P]),
     "nwk_chain_feed": (ctypes.c_int, [_P, _P, _P, _P, _I64]),
     "nwk_chain_finish": (ctypes.c_int, [_P, _P, _P, _P]),
@@ -93,8 +94,8 @@ _lib = None
 # per-launch counters (profiles/<round>/pmc_<workload>.json) can be tied to the
 # kernel build that produced them.
 KERNEL_SOURCES = {
-    "nw_align_bits": ("csrc/nwk_bits.hip", "csrc/nwk_internal.h", "Makefile"),
-    "nw_align_strip": ("csrc/nwk_bits.hip", "csrc/nwk_internal.h", "Makefile"),
+    "nw_align_bits": ("csrc/nwk_bits.hip", "csrc/nwk_sha_dev.h", "csrc/nwk_internal.h", "Makefile"),
+    "nw_align_strip": ("csrc/nwk_bits.hip", "csrc/nwk_sha_dev.h", "csrc/nwk_internal.h", "Makefile"),
     "nw_align_pka": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
     "nw_align_pk2": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
     "nw_align_pk": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
@@ -178,14 +179,16 @@ def pair_ij(p):
 class Engine:
     """One device context: pooled HBM workspace + streams (nwk_ctx)."""
 
-    FINALIZE = {"auto": 0, "host": 1, "device": 2}
+    FINALIZE = {"auto": 0, "host": 1, "device": 2, "fused": 3}
 
     KERNEL = {"auto": 0, "nw_align": 1, "nw_align_pk": 2, "nw_align_pk2": 3, "nw_align_bits": 4, "nw_align_strip": 5}
 
     def __init__(self, device=0, bits=0, workspace_bytes=0, host_threads=0, verbose=False, finalize="auto",
-                 linear_space=0, kernel="auto"):
+                 linear_space=0, kernel="auto", task_order=0):
         """finalize: where rows, penalty and SHA-512 of each pair are computed --
-        "auto" (per batch, by estimated cost), "host" threads, or "device" (nw_hash)."""
+        "auto" (per batch, by estimated cost), "host" threads, "device" (nw_rows +
+        nw_hash after each fill launch) or "fused" (inside the bits kernels' fill
+        launch, records streaming to the host as pairs finish: align_pairs_poll)."""
         self.lib = load_library()
         o = Opts()
         self.lib.nwk_opts_default(ctypes.byref(o))
@@ -197,6 +200,7 @@ class Engine:
         o.linear_space = linear_space
         # linear fill kernel (tests / A/B): "auto", "nw_align", "nw_align_pk", "nw_align_pk2", "nw_align_bits"
         o.kernel = self.KERNEL[kernel]
+        o.task_order = int(task_order)
         self._ctx = ctypes.c_void_p()
         _check(self.lib.nwk_ctx_create(ctypes.byref(o), ctypes.byref(self._ctx)))
         self.k = 0
@@ -241,6 +245,19 @@ class Engine:
         ids = np.ascontiguousarray(pair_ids, dtype=np.int64)
         _check(self.lib.nwk_align_pairs_begin(self._ctx, _ptr(ids), ids.size, pxy, pgap))
         self._pending = ids.size
+        self._poll_pen = np.zeros(max(ids.size, 1), dtype=np.int32)
+        self._poll_hs = np.zeros((max(ids.size, 1), 64), dtype=np.uint8)
+
+    def align_pairs_poll(self, start=0):
+        """While align_pairs_begin's call runs: (upto, penalties, hashes) of the
+        pairs pair_ids[start:upto] whose results are final (nwk_align_pairs_poll).
+        With the bits kernels' fused device finalize they stream in as each
+        pair's traceback ends; otherwise a batch's pairs arrive together."""
+        upto = ctypes.c_int64(0)
+        _check(self.lib.nwk_align_pairs_poll(self._ctx, int(start), _ptr(self._poll_pen), _ptr(self._poll_hs),
+                                             ctypes.addressof(upto)))
+        u = upto.value
+        return u, self._poll_pen[start:u].copy(), self._poll_hs[start:u].copy()
 
     def align_pairs_end(self):
         n = self._pending

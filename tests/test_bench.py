@@ -109,3 +109,18 @@ def test_bench_nccl_all_gather_at_world_one():
     if os.path.isdir(out):
         with open(os.path.join(out, "bench_nccl_world1.json"), "w") as f:
             f.write(json.dumps(line) + "\n")
+
+
+@pytest.mark.gpu
+def test_two_ranks_streamed_records_big13_published_hash():
+    """dist.align_sharded_streamed: one launch per rank (band tasks, pair-major),
+    four pieces exchanged as their records arrive, rank 0 chaining each piece."""
+    env = _env(NWK_BENCH_BACKEND="gloo", NWK_BENCH_SHARE_GPU="1", NWK_BENCH_WS_GB="110",
+                     NWK_BENCH_STREAM="1", NWK_BENCH_CHUNKS="4")
+    r = subprocess.run([sys.executable, "-u", BENCH, "--gpus", "2", "--workload", "big13",
+                        "--steps", "1", "--warmup", "0", "--no-cpu-baseline"], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, env=env, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.decode().strip().split("\n")[-1])
+    assert line["n_gpus"] == 2 and line["answer_hash_ok"] is True
+    assert "streamed" in line["config"]["parallelism"]

@@ -807,3 +807,43 @@ def test_driver_msa_fasta(golden, tmp_path):
     recs = seqalign.parse_fasta(out_fa.read_bytes())
     assert recs == rows
     assert out_fa.read_bytes().split(b"\n")[0] == b">seq0 sop=%d" % sop
+
+
+# --- fused device finalize + streamed records (nwk_align_pairs_poll) --------------------
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel,order", [("nw_align_bits", 1), ("nw_align_bits", 2), ("nw_align_strip", 0)])
+def test_fused_finalize_streamed_poll_vs_oracle(kernel, order):
+    """The bits kernels finalize each pair in the wave that traced it (rows,
+    penalty, problemhash -> host-mapped records); Engine.align_pairs_poll hands
+    out the final prefix while the call runs.  Every record against the oracle,
+    the prefix monotone, the end() result identical."""
+    r = random.Random(31 if kernel == "nw_align_bits" else 32)
+    lo, hi = (300, 3000) if kernel == "nw_align_bits" else (4100, 5200)  # strips: n / 64 >= 63
+    k = 24 if kernel == "nw_align_bits" else 6
+    genes = _rand_genes(r, k, lo, hi, ACGT)
+    ids = _all_ids(k)
+    with seqalign.Engine(device=0, finalize="fused", kernel=kernel, task_order=order) as e:
+        e.set_sequences(genes)
+        for pxy, pgap in ((3, 2), (5, 1)):
+            e.align_pairs_begin(ids, pxy, pgap)
+            pen = np.zeros(len(ids), dtype=np.int32)
+            hs = np.zeros((len(ids), 64), dtype=np.uint8)
+            got, seen = 0, []
+            while got < len(ids):
+                u, p_, h_ = e.align_pairs_poll(got)
+                assert u >= got
+                pen[got:u], hs[got:u] = p_, h_
+                if u > got:
+                    seen.append(u)
+                got = u
+            pe, he = e.align_pairs_end()
+            st = e.stats()
+            assert st["device_finalized"] == st["batches"]
+            oh, opens, ohs = oracle.all_pairs(genes, pxy, pgap)
+            assert [int(v) for v in pen] == opens
+            assert [h.tobytes().hex() for h in hs] == ohs
+            assert (pe == pen).all() and (he == hs).all()
+            assert seen[-1] == len(ids)
+

@@ -13,7 +13,7 @@ The all-gather of 72-byte records is not emulated (microseconds of transfer).
 W = 1 is the single-GPU getMinimumPenalties (align_all: batches with the chain
 overlapped), the bench's N=1 step.
 
-usage: python tools/shardtime.py [workload=big13] [--chunks C|auto] [W ...]   (workload: big13, c3, c4)"""
+usage: python tools/shardtime.py [workload=big13] [--chunks C|auto] [--stream] [W ...]   (workload: big13, c3, c4)"""
 import os
 import sys
 import time
@@ -28,6 +28,9 @@ import workloads  # noqa: E402
 args = sys.argv[1:]
 wl = args.pop(0) if args and not args[0].isdigit() and not args[0].startswith("--") else "big13"
 chunks_arg = "auto"
+stream = "--stream" in args  # one launch per rank, records polled as they stream (dist.align_sharded_streamed)
+if stream:
+    args.remove("--stream")
 if "--chunks" in args:
     i = args.index("--chunks")
     chunks_arg = args[i + 1]
@@ -51,6 +54,7 @@ tau = min((lambda: (lambda t0: (seqalign.chain_hash(rnd), time.perf_counter() - 
 print("%s: %d pairs; host chain %.1f ns per link (%.2f ms for all %d links)" % (wl, P, tau * 1e9, tau * P * 1e3, P),
       flush=True)
 
+es = None
 t1 = None
 for W in [int(a) for a in args] or [1, 2, 4, 8]:
     if W == 1:
@@ -64,6 +68,12 @@ for W in [int(a) for a in args] or [1, 2, 4, 8]:
         print("%s W=1: align_all %.2f ms (fill %.2f ms, %d batch(es), mode %s)" % (
             wl, best * 1e3, st["fill_ms"], st["batches"], seqalign.MODES.get(st["mode"])), flush=True)
         continue
+    if stream and es is None:  # records fused into the fill launch, polled as they stream (dist.align_sharded_streamed)
+        e.close()  # (its workspace holds most of the HBM)
+        es = seqalign.Engine(device=0, finalize="fused", kernel=os.environ.get("NWK_ST_KERNEL", "auto"),
+                             task_order=int(os.environ.get("NWK_ST_ORDER", "0")))
+        es.set_sequences(g)
+        es.align_pairs(np.arange(min(P, 64), dtype=np.int64), pxy, pgap)
     C = nwdist.auto_chunks(P, W) if chunks_arg == "auto" else int(chunks_arg)
     ready = np.zeros((W, C))
     links = np.zeros(C)
@@ -73,12 +83,25 @@ for W in [int(a) for a in args] or [1, 2, 4, 8]:
         for _ in range(3):
             t0 = time.perf_counter()
             ts = []
-            e.align_pairs_begin(parts[0], pxy, pgap)
-            for c in range(C):
-                e.align_pairs_end()
-                ts.append(time.perf_counter() - t0)
-                if c + 1 < C:
-                    e.align_pairs_begin(parts[c + 1], pxy, pgap)
+            if stream:
+                ids = np.concatenate(parts)
+                bounds = np.cumsum([len(x) for x in parts])
+                es.align_pairs_begin(ids, pxy, pgap)
+                got = 0
+                for c in range(C):
+                    while got < bounds[c]:
+                        got, _, _ = es.align_pairs_poll(got)
+                        if got < bounds[c]:
+                            time.sleep(50e-6)
+                    ts.append(time.perf_counter() - t0)
+                es.align_pairs_end()
+            else:
+                e.align_pairs_begin(parts[0], pxy, pgap)
+                for c in range(C):
+                    e.align_pairs_end()
+                    ts.append(time.perf_counter() - t0)
+                    if c + 1 < C:
+                        e.align_pairs_begin(parts[c + 1], pxy, pgap)
             if best is None or ts[-1] < best[-1]:
                 best = ts
         ready[r] = best
@@ -89,6 +112,6 @@ for W in [int(a) for a in args] or [1, 2, 4, 8]:
         end = max(end, ready[:, c].max()) + links[c] * tau
     fill_done = ready[:, -1].max()
     slow = int(np.argmax(ready[:, -1]))
-    print("%s W=%d, %d piece(s): slowest rank %d ready at %.2f ms (pieces %s ms); chain ends %.2f ms (exposed %.2f ms)%s"
-          % (wl, W, C, slow, fill_done * 1e3, " ".join("%.2f" % (x * 1e3) for x in ready[slow]), end * 1e3,
+    print("%s W=%d, %d piece(s)%s: slowest rank %d ready at %.2f ms (pieces %s ms); chain ends %.2f ms (exposed %.2f ms)%s"
+          % (wl, W, C, " streamed" if stream else "", slow, fill_done * 1e3, " ".join("%.2f" % (x * 1e3) for x in ready[slow]), end * 1e3,
              (end - fill_done) * 1e3, "  speedup vs W=1: %.2fx" % (t1 / end) if t1 else ""), flush=True)
