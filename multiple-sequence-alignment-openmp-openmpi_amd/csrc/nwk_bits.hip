@@ -604,44 +604,49 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
     if (wchk) {
       walk(std::true_type{});
     } else {
-      // The common case, ~35 scalar instructions a run: lanes past the stored
-      // steps are cut by one per-tile bound (LL), rows and columns by jb; the D
-      // lanes are not collected per run but rebuilt once from the stops below.
+      // The common case, ~28 scalar instructions a run.  The walk carries
+      // three lane bounds that a D run leaves unchanged: A = L + 2 (r - rowlo)
+      // (the tile's top row), B = L + 2 c (column 0) and LL (the last stored
+      // step); a U stop moves them by (-1, +1), an L stop by (+1, -1), and the
+      // key by (ls & 1) - [U].  r and c are recovered from A, B and L at the
+      // end.  The D lanes are not collected per run but rebuilt once from the
+      // stops below.
       const int LL = smin(63, ts - slo);  // last lane whose step is stored
       const int L0 = L;
       u64 vS = 0;  // lanes of the runs' stopping cells (U or L moves)
       int Kc = -(1 << 30);
-      u64 Dm = 0, Um = 0;
+      u64 SE = 0, SO = 0, Um = 0;  // the key's stops on even / odd lanes, its U cells
+      int A = L + 2 * (r - rowlo), B = L + 2 * c, K = r + (L >> 1);
       for (;;) {
-        const int jb = smin(r - rowlo, c);  // cells j <= jb keep row >= rowlo, column >= 0
-        if ((jb < 0) | (L > LL)) break;     // the current cell is outside the tile
+        const int bnd = smin(smin(A, B), LL);
+        if (L > bnd) break;  // the current cell is outside the tile
         ++n_runs;
-        const int K = r + (L >> 1);
         if (K != Kc) {
           const int i = K - Kb;
           if ((unsigned)i > 31u) break;  // off the key window: re-window (same tile)
-          Dm = __builtin_amdgcn_ballot_w64((WD >> i) & 1u);
+          const u64 Dm = __builtin_amdgcn_ballot_w64((WD >> i) & 1u);
           Um = __builtin_amdgcn_ballot_w64(!((WU >> i) & 1u));
+          SE = ~Dm & kEven;
+          SO = ~Dm & ~kEven;
           Kc = K;
         }
-        const int lend = L + 2 * smin(jb, (LL - L) >> 1) + 2;  // first lane past the readable cells
-        const u64 stops = ~Dm & ((L & 1) ? ~kEven : kEven) & (~0ull << L);
+        const int lend = L + ((bnd - L) & ~1) + 2;  // first lane past the readable cells
+        const u64 stops = ((L & 1) ? SO : SE) & (~0ull << L);
         const int ls = sminu(sff1(stops), lend);  // (no stop: ff1 = -1)
-        const int jn = (ls - L) >> 1;
-        r -= jn;
-        c -= jn;
         if (ls >= lend) {  // the run leaves the tile
-          L = ls;
+          L = lend;
           break;
         }
-        const u64 bit = 1ull << ls;
-        vS |= bit;
-        const int u = (Um & bit) ? 1 : 0;
-        vU |= u ? bit : 0ull;
-        r -= u;
-        c -= 1 - u;
+        vS |= 1ull << ls;
+        const int u = (int)((Um >> ls) & 1ull);
+        vU |= (u64)u << ls;
+        A += 1 - 2 * u;
+        B += 2 * u - 1;
+        K += (ls & 1) - u;
         L = ls + 1;
       }
+      r = rowlo + ((A - L) >> 1);
+      c = (B - L) >> 1;
       // D lanes: in [L0, L), not a stop, an even offset from the start of their run
       const u64 starts = (1ull << L0) | (vS << 1);
       const u64 sb = (starts & ((2ull << lane) - 1)) | 1ull;
@@ -937,7 +942,10 @@ __device__ __forceinline__ void hq_drain(const FillArgs& a, int lane) {
 #define NWK_BITS_OCC
 #endif
 
-template <int NP, int SR>
+// FUSE: the instantiation with the fused finalize (FillArgs::fuse_fin); the
+// plain one carries none of its code, so the hashing's registers never touch
+// the fill and trace (one instantiation with both: lone C3 trace 4.7 -> 5.8 ms)
+template <int NP, int SR, bool FUSE>
 __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned cons_all[4][64 * NP];
   __shared__ __attribute__((aligned(16))) unsigned ring_all[4][128 * NP];
@@ -952,7 +960,7 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
   if (a.stamps && threadIdx.x == 0) atomicMin(a.stamps + 11 * a.ntasks_pairs, (u64)__builtin_amdgcn_s_memrealtime());
 
   for (;;) {
-    if (a.fuse_fin) {  // queued pairs to hash: whole groups between fill tasks
+    if constexpr (FUSE) {  // queued pairs to hash: whole groups between fill tasks
       while (hq_hash(a, lane, false)) {
       }
     }
@@ -961,7 +969,7 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
     tk = __builtin_amdgcn_readfirstlane(tk);
     BITS_PROG(0x10000000u | tk);
     if (tk >= (unsigned)a.ntasks) {
-      if (a.fuse_fin) hq_drain(a, lane);
+      if constexpr (FUSE) hq_drain(a, lane);
       BITS_PROG(0x60000000u);
       return;
     }
@@ -1121,7 +1129,7 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
 #if NWK_TRACE_PRIO
       __builtin_amdgcn_s_setprio(0);
 #endif
-      if (a.fuse_fin) {
+      if constexpr (FUSE) {
         if (!tout) fin_rows(a, pd, lane, tlen, tend);
         hq_push(a, pd, lane, !tout);
       }
@@ -1158,7 +1166,7 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
 // bit-reversed (bit b = row 32 lane + b).  Storage: the strip's 8-step blocks
 // in order (full), or per band the blocks strip_blk_lo(band) .. + nblk of its
 // W-column diagonal window (the runtime keeps the bands' windows disjoint).
-template <int NP, int SR>
+template <int NP, int SR, bool FUSE>
 __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned cons_all[4][64 * NP];
   __shared__ __attribute__((aligned(16))) unsigned ring_all[4][128 * NP];
@@ -1173,7 +1181,7 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
   constexpr int NG = 2 * NP;  // packed dwords per 64-column chunk of a pass's last row
 
   for (;;) {
-    if (a.fuse_fin) {
+    if constexpr (FUSE) {
       while (hq_hash(a, lane, false)) {
       }
     }
@@ -1182,7 +1190,7 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
     tk = __builtin_amdgcn_readfirstlane(tk);
     BITS_PROG(0x10000000u | tk);
     if (tk >= (unsigned)a.ntasks) {
-      if (a.fuse_fin) hq_drain(a, lane);
+      if constexpr (FUSE) hq_drain(a, lane);
       BITS_PROG(0x60000000u);
       return;
     }
@@ -1326,7 +1334,7 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
     int2 tend;
     bool tout;
     trace_bits(a, pd, obuf_all[wid], lane, prog, tlen, tend, tout);
-    if (a.fuse_fin) {
+    if constexpr (FUSE) {
       if (!tout) fin_rows(a, pd, lane, tlen, tend);
       hq_push(a, pd, lane, !tout);
     }
@@ -1337,20 +1345,22 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
 
 template <int NP, int SR>
 hipError_t bits_launch(const FillArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((nw_align_bits<NP, SR>), dim3(grid), dim3(256), 0, s, a);
+  if (a.fuse_fin) hipLaunchKernelGGL((nw_align_bits<NP, SR, true>), dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((nw_align_bits<NP, SR, false>), dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 template <int NP, int SR>
 hipError_t strip_launch(const FillArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((nw_align_strip<NP, SR>), dim3(grid), dim3(256), (size_t)4 * a.strip_ring * 4, s, a);
+  if (a.fuse_fin) hipLaunchKernelGGL((nw_align_strip<NP, SR, true>), dim3(grid), dim3(256), (size_t)4 * a.strip_ring * 4, s, a);
+  else hipLaunchKernelGGL((nw_align_strip<NP, SR, false>), dim3(grid), dim3(256), (size_t)4 * a.strip_ring * 4, s, a);
   return hipGetLastError();
 }
 
 template <int NP, int SR>
 int strip_occ(int ring_dwords) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&nw_align_strip<NP, SR>), 256,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&nw_align_strip<NP, SR, false>), 256,
                                                    (size_t)4 * ring_dwords * 4) != hipSuccess)
     return 1;
   return n > 0 ? n : 1;
@@ -1359,7 +1369,7 @@ int strip_occ(int ring_dwords) {
 template <int NP, int SR>
 int bits_occ() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&nw_align_bits<NP, SR>), 256, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&nw_align_bits<NP, SR, false>), 256, 0) !=
       hipSuccess)
     return 1;
   return n > 0 ? n : 1;
