@@ -1016,6 +1016,12 @@ bool use_strips(const nwk_ctx* c, const std::vector<PairWork>& work, int pgap, b
     std::push_heap(heap.begin(), heap.end(), std::greater<int64_t>());
   }
   const double est_s = (double)*std::max_element(heap.begin(), heap.end());
+  // Beyond two rounds of strips per wave slot the band tasks keep every slot
+  // busy too, and a strip step costs more than a band step (pass switches,
+  // per-lane storage window): C4 on one GPU (8 rounds) fills in 86.8 ms as
+  // bands vs 88.7 ms as strips, 100.9 vs 104.8 ms per step; a C4 shard of 8
+  // ranks (1 round) stays on strips (14.5 vs 21.7 ms).
+  if (npairs > 2 * slots_s) return est_s < 0.8 * est_b;
   return est_s < 0.95 * est_b;
 }
 
