@@ -77,31 +77,66 @@ void compress(uint64_t st[8], const unsigned char* blk) {
   st[0] += a; st[1] += b; st[2] += c; st[3] += d;
   st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
+// The chain's rounds (latency-bound: one dependent compression after another).
+// Maj(a, b, c) = b ^ ((a ^ b) & (b ^ c)) with (b ^ c) carried over from the
+// previous round's (a ^ b), and h + K + W summed off the e / a critical paths:
+// 354 vs 400 ns per chain link on the MI355X box's EPYC 9575F
+// (tools/probe/chain_probe2.cpp).
+#define NWK_RC(a, b, c, d, e, f, g, h, kw, AB, BC)                      \
+  do {                                                                \
+    const uint64_t t1 = (h + (kw)) + (g ^ (e & (f ^ g))) + NWK_S1(e); \
+    AB = a ^ b;                                                       \
+    d += t1;                                                          \
+    h = t1 + (NWK_S0(a) + (b ^ (AB & BC)));                           \
+  } while (0)
+
 // Compression over a precomputed K + W schedule (the chain's fixed blocks).
 void compress_kw(uint64_t st[8], const uint64_t kw[80]) {
   uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#define NWK_RKW(a, b, c, d, e, f, g, h, t)                                      \
-  do {                                                                        \
-    const uint64_t t1 = h + NWK_S1(e) + (g ^ (e & (f ^ g))) + kw[t];           \
-    const uint64_t t2 = NWK_S0(a) + ((a & b) | (c & (a | b)));                \
-    d += t1;                                                                  \
-    h = t1 + t2;                                                              \
-  } while (0)
+  uint64_t x = b ^ c, y;
 #pragma unroll
   for (int t = 0; t < 80; t += 8) {
-    NWK_RKW(a, b, c, d, e, f, g, h, t + 0);
-    NWK_RKW(h, a, b, c, d, e, f, g, t + 1);
-    NWK_RKW(g, h, a, b, c, d, e, f, t + 2);
-    NWK_RKW(f, g, h, a, b, c, d, e, t + 3);
-    NWK_RKW(e, f, g, h, a, b, c, d, t + 4);
-    NWK_RKW(d, e, f, g, h, a, b, c, t + 5);
-    NWK_RKW(c, d, e, f, g, h, a, b, t + 6);
-    NWK_RKW(b, c, d, e, f, g, h, a, t + 7);
+    NWK_RC(a, b, c, d, e, f, g, h, kw[t + 0], y, x);
+    NWK_RC(h, a, b, c, d, e, f, g, kw[t + 1], x, y);
+    NWK_RC(g, h, a, b, c, d, e, f, kw[t + 2], y, x);
+    NWK_RC(f, g, h, a, b, c, d, e, kw[t + 3], x, y);
+    NWK_RC(e, f, g, h, a, b, c, d, kw[t + 4], y, x);
+    NWK_RC(d, e, f, g, h, a, b, c, kw[t + 5], x, y);
+    NWK_RC(c, d, e, f, g, h, a, b, kw[t + 6], y, x);
+    NWK_RC(b, c, d, e, f, g, h, a, kw[t + 7], x, y);
   }
-#undef NWK_RKW
   st[0] += a; st[1] += b; st[2] += c; st[3] += d;
   st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
+
+// Compression of a block given as 16 big-endian words, its schedule rolled
+// into the rounds (the chain's first block, hex(acc): no schedule pass ahead
+// of the rounds on the link's critical path)
+void compress_w16(uint64_t st[8], uint64_t w[16]) {
+  uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+  uint64_t x = b ^ c, y;
+#pragma unroll
+  for (int t = 0; t < 80; t += 8) {
+    if (t >= 16) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int u = t + q;
+        w[u & 15] += NWK_s1(w[(u - 2) & 15]) + w[(u - 7) & 15] + NWK_s0(w[(u - 15) & 15]);
+      }
+    }
+    NWK_RC(a, b, c, d, e, f, g, h, kK[t + 0] + w[(t + 0) & 15], y, x);
+    NWK_RC(h, a, b, c, d, e, f, g, kK[t + 1] + w[(t + 1) & 15], x, y);
+    NWK_RC(g, h, a, b, c, d, e, f, kK[t + 2] + w[(t + 2) & 15], y, x);
+    NWK_RC(f, g, h, a, b, c, d, e, kK[t + 3] + w[(t + 3) & 15], x, y);
+    NWK_RC(e, f, g, h, a, b, c, d, kK[t + 4] + w[(t + 4) & 15], y, x);
+    NWK_RC(d, e, f, g, h, a, b, c, kK[t + 5] + w[(t + 5) & 15], x, y);
+    NWK_RC(c, d, e, f, g, h, a, b, kK[t + 6] + w[(t + 6) & 15], y, x);
+    NWK_RC(b, c, d, e, f, g, h, a, kK[t + 7] + w[(t + 7) & 15], x, y);
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+  st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+#undef NWK_RC
 
 // K + W of a block given as 16 big-endian words
 void schedule_kw(const uint64_t w16[16], uint64_t kw[80]) {
@@ -174,10 +209,9 @@ void chain_step(ChainAcc* acc, const uint64_t kw[80]) {
     compress_kw(st, pad_kw().kw128);
     acc->empty = false;
   } else {           // message = hex(acc) ++ hex(ph), then the padding of a 256-byte message
-    uint64_t w16[16], kw1[80];
+    uint64_t w16[16];
     hex_block(acc->dig, w16);
-    schedule_kw(w16, kw1);
-    compress_kw(st, kw1);
+    compress_w16(st, w16);
     compress_kw(st, kw);
     compress_kw(st, pad_kw().kw256);
   }
