@@ -13,7 +13,7 @@ The all-gather of 72-byte records is not emulated (microseconds of transfer).
 W = 1 is the single-GPU getMinimumPenalties (align_all: batches with the chain
 overlapped), the bench's N=1 step.
 
-usage: python tools/shardtime.py [workload=big13] [--chunks C|auto] [--stream] [W ...]   (workload: big13, c3, c4)"""
+usage: [NWK_ST_LIB=lib] python tools/shardtime.py [workload=big13] [--chunks C|auto] [--stream] [W ...]   (workload: big13, c3, c4)"""
 import os
 import sys
 import time
@@ -41,6 +41,8 @@ if wl == "big13":
 else:
     _, k, L, pxy, pgap, _ = workloads.SYNTH[wl]
     g = workloads.synth(k, L)
+if os.environ.get("NWK_ST_LIB"):  # A/B: a libnwk.so variant (tools/abv/<name>/libnwk.so)
+    seqalign.load_library(os.environ["NWK_ST_LIB"])
 lens = [len(s) for s in g]
 P = len(g) * (len(g) - 1) // 2
 e = seqalign.Engine(device=0)
