@@ -13,7 +13,7 @@ The all-gather of 72-byte records is not emulated (microseconds of transfer).
 W = 1 is the single-GPU getMinimumPenalties (align_all: batches with the chain
 overlapped), the bench's N=1 step.
 
-usage: [NWK_ST_LIB=lib] python tools/shardtime.py [workload=big13] [--chunks C|auto] [--stream] [W ...]   (workload: big13, c3, c4)"""
+usage: [NWK_ST_LIB=lib] python tools/shardtime.py [workload=big13] [--chunks C|auto] [--stream [--hybrid H]] [W ...]   (workload: big13, c3, c4)"""
 import os
 import sys
 import time
@@ -31,6 +31,11 @@ chunks_arg = "auto"
 stream = "--stream" in args  # one launch per rank, records polled as they stream (dist.align_sharded_streamed)
 if stream:
     args.remove("--stream")
+hybrid = 0  # --hybrid H: the first H pieces as band tasks (nw_align_bits, pair-major) in a launch of their own beside the strips
+if "--hybrid" in args:
+    i = args.index("--hybrid")
+    hybrid = int(args[i + 1])
+    del args[i:i + 2]
 if "--chunks" in args:
     i = args.index("--chunks")
     chunks_arg = args[i + 1]
@@ -73,9 +78,14 @@ for W in [int(a) for a in args] or [1, 2, 4, 8]:
     if stream and es is None:  # records fused into the fill launch, polled as they stream (dist.align_sharded_streamed)
         e.close()  # (its workspace holds most of the HBM)
         es = seqalign.Engine(device=0, finalize="fused", kernel=os.environ.get("NWK_ST_KERNEL", "auto"),
-                             task_order=int(os.environ.get("NWK_ST_ORDER", "0")))
+                             task_order=int(os.environ.get("NWK_ST_ORDER", "0")), workspace_bytes=(100 << 30) if hybrid else 0)
         es.set_sequences(g)
         es.align_pairs(np.arange(min(P, 64), dtype=np.int64), pxy, pgap)
+        if hybrid:
+            eh = seqalign.Engine(device=0, finalize="fused", kernel="nw_align_bits", task_order=1,
+                                 workspace_bytes=60 << 30)
+            eh.set_sequences(g)
+            eh.align_pairs(np.arange(min(P, 64), dtype=np.int64), pxy, pgap)
     C = nwdist.auto_chunks(P, W) if chunks_arg == "auto" else int(chunks_arg)
     ready = np.zeros((W, C))
     links = np.zeros(C)
@@ -85,7 +95,25 @@ for W in [int(a) for a in args] or [1, 2, 4, 8]:
         for _ in range(3):
             t0 = time.perf_counter()
             ts = []
-            if stream:
+            if stream and hybrid:
+                ia, ib = np.concatenate(parts[:hybrid]), np.concatenate(parts[hybrid:])
+                eh.align_pairs_begin(ia, pxy, pgap)
+                es.align_pairs_begin(ib, pxy, pgap)
+                bounds = np.cumsum([len(x) for x in parts])
+                ga = gb = 0
+                for c in range(C):
+                    eng, tgt = (eh, bounds[c]) if c < hybrid else (es, bounds[c] - len(ia))
+                    while (ga if c < hybrid else gb) < tgt:
+                        if c < hybrid:
+                            ga, _, _ = eng.align_pairs_poll(ga)
+                        else:
+                            gb, _, _ = eng.align_pairs_poll(gb)
+                        if (ga if c < hybrid else gb) < tgt:
+                            time.sleep(50e-6)
+                    ts.append(time.perf_counter() - t0)
+                eh.align_pairs_end()
+                es.align_pairs_end()
+            elif stream:
                 ids = np.concatenate(parts)
                 bounds = np.cumsum([len(x) for x in parts])
                 es.align_pairs_begin(ids, pxy, pgap)
@@ -115,5 +143,5 @@ for W in [int(a) for a in args] or [1, 2, 4, 8]:
     fill_done = ready[:, -1].max()
     slow = int(np.argmax(ready[:, -1]))
     print("%s W=%d, %d piece(s)%s: slowest rank %d ready at %.2f ms (pieces %s ms); chain ends %.2f ms (exposed %.2f ms)%s"
-          % (wl, W, C, " streamed" if stream else "", slow, fill_done * 1e3, " ".join("%.2f" % (x * 1e3) for x in ready[slow]), end * 1e3,
+          % (wl, W, C, (" streamed" + (" (%d band-task)" % hybrid if hybrid else "")) if stream else "", slow, fill_done * 1e3, " ".join("%.2f" % (x * 1e3) for x in ready[slow]), end * 1e3,
              (end - fill_done) * 1e3, "  speedup vs W=1: %.2fx" % (t1 / end) if t1 else ""), flush=True)
