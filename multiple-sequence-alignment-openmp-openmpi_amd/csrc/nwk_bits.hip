@@ -716,13 +716,15 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
 
 // align1 / align2 (skel:263-272 prefix, then the moves in forward order: 64
 // per iteration, a wave scan of the packed x / y advances) and the path cost
-// (= dp[m][n], the reference's penalty) -> fin_len[slot], fin_len[np + slot]
-__device__ __forceinline__ void fin_rows(const FillArgs& a, const PairDesc& pd, int lane, int nops, int2 e) {
+// (= dp[m][n], the reference's penalty) -> fin_len[slot], fin_len[np + slot].
+// Returns false when the walk or its moves are inconsistent (error word set):
+// the pair is then not queued, so no record with stale rows is ever published.
+__device__ __forceinline__ bool fin_rows(const FillArgs& a, const PairDesc& pd, int lane, int nops, int2 e) {
   using namespace shadev;
   const int pre = e.x > 0 ? e.x : e.y;
   if (e.x < 0 || e.y < 0 || e.x > pd.m || e.y > pd.n || nops < 0 || pre + nops > pd.m + pd.n) {
     if (lane == 0) atomicOr(a.err, 128u);  // (a walk that did not end on the border)
-    return;
+    return false;
   }
   const uint8_t* ops = a.ops + pd.ops_off;
   const uint8_t* x = a.raw + pd.x_off;
@@ -735,6 +737,7 @@ __device__ __forceinline__ void fin_rows(const FillArgs& a, const PairDesc& pd, 
   }
   int ix = e.x, iy = e.y;
   int pen = 0;
+  bool off = false;  // a move left the matrix
   for (int base = 0; base < nops; base += 64) {
     const int f = base + lane;
     const bool live = f < nops;
@@ -748,6 +751,7 @@ __device__ __forceinline__ void fin_rows(const FillArgs& a, const PairDesc& pd, 
       const int xi = ix + (int)(exc & 0xffffu), yi = iy + (int)(exc >> 16);
       if ((ax && xi >= pd.m) || (ay && yi >= pd.n)) {
         atomicOr(a.err, 256u);  // (moves that leave the matrix)
+        off = true;
       } else {
         const unsigned chx = ax ? x[xi] : (unsigned)'_';
         const unsigned chy = ay ? y[yi] : (unsigned)'_';
@@ -766,6 +770,7 @@ __device__ __forceinline__ void fin_rows(const FillArgs& a, const PairDesc& pd, 
     a.fin_len[pd.slot] = pre + nops;  // both rows have this length
     a.fin_len[a.ntasks_pairs + pd.slot] = pen + pre * a.pgap;
   }
+  return !__any(off);
 }
 
 // After fin_rows: publish the rows (a hashing wave may run on another XCD)
@@ -1130,8 +1135,8 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
       __builtin_amdgcn_s_setprio(0);
 #endif
       if constexpr (FUSE) {
-        if (!tout) fin_rows(a, pd, lane, tlen, tend);
-        hq_push(a, pd, lane, !tout);
+        const bool ok_rows = !tout && fin_rows(a, pd, lane, tlen, tend);
+        hq_push(a, pd, lane, ok_rows);
       }
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
       BITS_PROG(0x56000000u);
@@ -1335,8 +1340,8 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
     bool tout;
     trace_bits(a, pd, obuf_all[wid], lane, prog, tlen, tend, tout);
     if constexpr (FUSE) {
-      if (!tout) fin_rows(a, pd, lane, tlen, tend);
-      hq_push(a, pd, lane, !tout);
+      const bool ok_rows = !tout && fin_rows(a, pd, lane, tlen, tend);
+      hq_push(a, pd, lane, ok_rows);
     }
     if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
     BITS_PROG(0x56000000u);

@@ -25,6 +25,7 @@
 #include <memory>
 #include <string>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 #include <unistd.h>
 
@@ -2124,8 +2125,11 @@ int nwk_chain_create(int64_t P, nwk_chain** out) {
 int nwk_chain_feed(nwk_chain* ch, const int64_t* ids, const int32_t* penalties, const uint8_t* problem_hash,
                    int64_t n) {
   if (!ch || n < 0 || (n > 0 && (!ids || !problem_hash))) return fail(NWK_EINVAL, "nwk_chain_feed: bad argument");
+  // each id once: against earlier calls (ready) and within this batch (seen)
+  std::unordered_set<int64_t> seen;
+  seen.reserve((size_t)n);
   for (int64_t q = 0; q < n; ++q)
-    if (ids[q] < 0 || ids[q] >= ch->P || ch->ready[ids[q]].load(std::memory_order_relaxed))
+    if (ids[q] < 0 || ids[q] >= ch->P || ch->ready[ids[q]].load(std::memory_order_relaxed) || !seen.insert(ids[q]).second)
       return fail(NWK_EINVAL, "nwk_chain_feed: pair id %lld out of range or fed twice", (long long)ids[q]);
   for (int64_t q = 0; q < n; ++q) {
     const int64_t p = ids[q];

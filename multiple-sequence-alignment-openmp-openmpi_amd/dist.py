@@ -117,123 +117,145 @@ def auto_chunks(P, world):
     return 1
 
 
-def align_sharded_pipelined(eng, lengths, pxy, pgap, rank, world, chunks=1, device=None, group=None,
-                            on_piece=None):
-    """The shard in `chunks` pieces of ascending canonical ids: piece c+1 aligns
-    on the GPU (Engine.align_pairs_begin) while piece c's records go through
-    their all-gather and rank 0's chain worker (seqalign.ChainStream) advances
-    over them -- sub:305-337 collects results as they arrive and then chains;
-    here the chain of all but the last piece hides behind the alignment.
-    Returns (hash on rank 0 else None, penalties[P], hashes[P,64]) on rank 0,
-    (None, None, None) elsewhere.  Same failure contract as align_sharded:
-    a failing rank joins every remaining collective with FAILED records."""
-    k = len(lengths)
-    P = k * (k - 1) // 2
-    parts, per = chunk_parts(lengths, rank, world, chunks)
-    chain = seqalign.ChainStream(P) if rank == 0 else None
-    err = None       # this rank's failure, or a peer's seen in a gather
-    pending = False  # an align_pairs_begin not yet ended
-    try:
+def failed_block(per):
+    """A padded record block with every record tagged FAILED."""
+    rec = pack_records([], [], [], per)
+    rec[:, :4] = np.array([FAILED], dtype=np.int32).view(np.uint8)
+    return rec
+
+
+class PipelinedShard:
+    """Rank side of align_sharded_pipelined: the shard in pieces of ascending
+    canonical ids, piece c+1 aligning (Engine.align_pairs_begin) while piece
+    c's block is exchanged.  block(c) returns piece c's padded record block --
+    FAILED-tagged once this rank has failed, so it still joins every
+    collective.  The tests and tools/shardtime.py drive the same object per
+    rank on one GPU and stand in for the all-gather with a concatenation."""
+
+    def __init__(self, eng, parts, per, pxy, pgap, on_piece=None):
+        self.eng, self.parts, self.per, self.pxy, self.pgap = eng, parts, per, pxy, pgap
+        self.on_piece = on_piece
+        self.err = None       # this rank's own failure
+        self.pending = False  # an align_pairs_begin not yet ended
+
+    def start(self):
         try:
-            eng.align_pairs_begin(parts[0], pxy, pgap)
-            pending = True
+            self.eng.align_pairs_begin(self.parts[0], self.pxy, self.pgap)
+            self.pending = True
         except Exception as e:
-            err = e
-        for c in range(chunks):
-            rec = None
-            if err is None:
-                try:
-                    pending = False
-                    pen, hs = eng.align_pairs_end()
-                    if on_piece is not None:
-                        on_piece(c)
-                    if c + 1 < chunks:
-                        eng.align_pairs_begin(parts[c + 1], pxy, pgap)
-                        pending = True
-                    rec = pack_records(parts[c], pen, hs, per[c])
-                except Exception as e:
-                    err = e
-            if rec is None:  # still join the collective, so no peer waits forever
-                rec = pack_records([], [], [], per[c])
-                rec[:, :4] = np.array([FAILED], dtype=np.int32).view(np.uint8)
-            g = all_gather_records(rec, device=device, group=group)
-            if err is not None:
-                continue
+            self.err = e
+
+    def block(self, c):
+        if self.err is None:
             try:
-                ids, pen, hs = unpack_chunk(g)
-            except RankFailed as e:  # every rank sees it in the same gather
-                err = e
-                continue
-            if chain is not None:
-                chain.feed(ids, pen, hs)
-        if err is not None:
-            raise RankFailed("rank %d: %s" % (rank, err)) from err
-        if chain is None:
-            return None, None, None
-        return chain.finish()
-    finally:
-        if pending:  # a peer failed while this rank's next piece was in flight
+                self.pending = False
+                pen, hs = self.eng.align_pairs_end()
+                if self.on_piece is not None:
+                    self.on_piece(c)
+                if c + 1 < len(self.parts):
+                    self.eng.align_pairs_begin(self.parts[c + 1], self.pxy, self.pgap)
+                    self.pending = True
+                return pack_records(self.parts[c], pen, hs, self.per[c])
+            except Exception as e:
+                self.err = e
+        return failed_block(self.per[c])
+
+    def finish(self):
+        """Ends a call still in flight (a peer failed first); returns this rank's error."""
+        if self.pending:
+            self.pending = False
             try:
-                eng.align_pairs_end()
+                self.eng.align_pairs_end()
             except Exception:
                 pass
-        if chain is not None:
-            chain.close()
+        return self.err
 
 
-def align_sharded_streamed(eng, lengths, pxy, pgap, rank, world, chunks=8, device=None, group=None,
-                           on_piece=None, poll_s=50e-6):
-    """The shard as ONE launch (Engine.align_pairs_begin over its ids in
-    ascending canonical order, the engine built with finalize="fused") whose
-    per-pair records stream to the host as pairs are hashed inside the fill
-    launch (Engine.align_pairs_poll).
-    Piece c -- the shard's ids below the global threshold P (c+1) / chunks --
-    goes through its all-gather as soon as all of its records are in, and rank
-    0's chain worker advances over it while the rest of the shard still
-    aligns: sub:305-331 collects results as they arrive, sub:334-337 chains.
-    Same return value and failure contract as align_sharded_pipelined."""
-    import time
+class StreamedShard:
+    """Rank side of align_sharded_streamed: the whole shard as ONE launch over
+    its ids in ascending canonical order (the engine built with
+    finalize="fused"), its per-pair records polled as they stream out of the
+    fill launch (Engine.align_pairs_poll).  block(c) waits until every record
+    of piece c is in and returns its padded block (FAILED-tagged once this
+    rank has failed).  finish() ends the launch: errors that only the end of
+    the call reports (the device error word, a fused record that fails its
+    checks) surface there, after every piece's exchange -- hence the final
+    status collective in align_sharded_streamed."""
 
-    k = len(lengths)
-    P = k * (k - 1) // 2
-    parts, per = chunk_parts(lengths, rank, world, chunks)
-    ids = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int64)
-    bounds = np.cumsum([0] + [len(x) for x in parts])
-    chain = seqalign.ChainStream(P) if rank == 0 else None
-    pen = np.zeros(max(len(ids), 1), dtype=np.int32)
-    hs = np.zeros((max(len(ids), 1), 64), dtype=np.uint8)
-    err = None
-    pending = False
-    got = 0
-    try:
+    def __init__(self, eng, parts, per, pxy, pgap, poll_s=50e-6, on_piece=None):
+        self.eng, self.parts, self.per, self.pxy, self.pgap = eng, parts, per, pxy, pgap
+        self.poll_s, self.on_piece = poll_s, on_piece
+        self.ids = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int64)
+        self.bounds = np.cumsum([0] + [len(x) for x in parts])
+        n = max(len(self.ids), 1)
+        self.pen = np.zeros(n, dtype=np.int32)
+        self.hs = np.zeros((n, 64), dtype=np.uint8)
+        self.got = 0
+        self.err = None
+        self.pending = False
+
+    def start(self):
         try:
-            eng.align_pairs_begin(ids, pxy, pgap)
-            pending = True
+            self.eng.align_pairs_begin(self.ids, self.pxy, self.pgap)
+            self.pending = True
         except Exception as e:
-            err = e
+            self.err = e
+
+    def block(self, c):
+        import time
+
+        if self.err is None:
+            try:
+                hi = self.bounds[c + 1]
+                while self.got < hi:
+                    u, p_, h_ = self.eng.align_pairs_poll(self.got)
+                    if u > self.got:
+                        self.pen[self.got:u] = p_
+                        self.hs[self.got:u] = h_
+                        self.got = u
+                    elif self.got < hi:
+                        time.sleep(self.poll_s)
+                if self.on_piece is not None:
+                    self.on_piece(c)
+                lo = self.bounds[c]
+                return pack_records(self.parts[c], self.pen[lo:hi], self.hs[lo:hi], self.per[c])
+            except Exception as e:
+                self.err = e
+        return failed_block(self.per[c])
+
+    def finish(self):
+        """Ends the launch; returns this rank's error (None on success)."""
+        if self.pending:
+            self.pending = False
+            try:
+                self.eng.align_pairs_end()
+            except Exception as e:
+                if self.err is None:
+                    self.err = e
+        return self.err
+
+
+def any_rank_failed(failed, device=None, group=None):
+    """One status collective (all_reduce MAX of a flag): True on every rank
+    when any rank failed."""
+    import torch
+
+    t = torch.tensor([1 if failed else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return bool(int(t.item()))
+
+
+def _exchange(shard, chunks, rank, P, device, group, final_status):
+    """The collective side shared by both pipelines: one all-gather per piece,
+    rank 0's chain worker fed per piece as it arrives (sub:305-331 collects
+    results as they arrive, sub:334-337 chains)."""
+    chain = seqalign.ChainStream(P) if rank == 0 else None
+    err = None  # a peer's failure seen in a gather
+    try:
+        shard.start()
         for c in range(chunks):
-            rec = None
-            if err is None:
-                try:
-                    while got < bounds[c + 1]:
-                        u, p_, h_ = eng.align_pairs_poll(got)
-                        if u > got:
-                            pen[got:u] = p_
-                            hs[got:u] = h_
-                            got = u
-                        elif got < bounds[c + 1]:
-                            time.sleep(poll_s)
-                    if on_piece is not None:
-                        on_piece(c)
-                    lo, hi = bounds[c], bounds[c + 1]
-                    rec = pack_records(parts[c], pen[lo:hi], hs[lo:hi], per[c])
-                except Exception as e:
-                    err = e
-            if rec is None:  # still join the collective, so no peer waits forever
-                rec = pack_records([], [], [], per[c])
-                rec[:, :4] = np.array([FAILED], dtype=np.int32).view(np.uint8)
-            g = all_gather_records(rec, device=device, group=group)
-            if err is not None:
+            g = all_gather_records(shard.block(c), device=device, group=group)
+            if err is not None or shard.err is not None:
                 continue
             try:
                 cid, cpen, chs = unpack_chunk(g)
@@ -242,26 +264,86 @@ def align_sharded_streamed(eng, lengths, pxy, pgap, rank, world, chunks=8, devic
                 continue
             if chain is not None:
                 chain.feed(cid, cpen, chs)
-        if pending:
-            pending = False
-            try:
-                eng.align_pairs_end()
-            except Exception as e:
-                if err is None:
-                    err = e
+        own = shard.finish()
+        err = own if own is not None else err
+        if final_status and any_rank_failed(err is not None, device=device, group=group) and err is None:
+            err = RankFailed("a peer rank failed after the last piece was exchanged")
         if err is not None:
             raise RankFailed("rank %d: %s" % (rank, err)) from err
         if chain is None:
             return None, None, None
         return chain.finish()
     finally:
-        if pending:
-            try:
-                eng.align_pairs_end()
-            except Exception:
-                pass
+        shard.finish()
         if chain is not None:
             chain.close()
+
+
+def align_sharded_pipelined(eng, lengths, pxy, pgap, rank, world, chunks=1, device=None, group=None,
+                            on_piece=None):
+    """The shard in `chunks` pieces of ascending canonical ids: piece c+1 aligns
+    on the GPU (Engine.align_pairs_begin) while piece c's records go through
+    their all-gather and rank 0's chain worker (seqalign.ChainStream) advances
+    over them -- sub:305-337 collects results as they arrive and then chains;
+    here the chain of all but the last piece hides behind the alignment.
+    Returns (hash, penalties[P], hashes[P,64]) on rank 0, (None, None, None)
+    elsewhere.  Same failure contract as align_sharded: a failing rank joins
+    every remaining collective with FAILED records, and every rank raises
+    (each piece's end() runs before its gather, so no final status is needed)."""
+    k = len(lengths)
+    P = k * (k - 1) // 2
+    parts, per = chunk_parts(lengths, rank, world, chunks)
+    shard = PipelinedShard(eng, parts, per, pxy, pgap, on_piece=on_piece)
+    return _exchange(shard, chunks, rank, P, device, group, final_status=False)
+
+
+def align_sharded_streamed(eng, lengths, pxy, pgap, rank, world, chunks=8, device=None, group=None,
+                           on_piece=None, poll_s=50e-6):
+    """The shard as ONE launch whose per-pair records stream to the host as
+    pairs are hashed inside the fill launch (StreamedShard).  Piece c -- the
+    shard's ids below the global threshold P (c+1) / chunks -- goes through its
+    all-gather as soon as all of its records are in, and rank 0's chain worker
+    advances over it while the rest of the shard still aligns.
+    Same return value and failure contract as align_sharded_pipelined, plus one
+    status collective after the launch has ended: a rank whose failure only the
+    end of its call reports (after its records were already exchanged) makes
+    every rank, rank 0 included, raise instead of returning a hash."""
+    k = len(lengths)
+    P = k * (k - 1) // 2
+    parts, per = chunk_parts(lengths, rank, world, chunks)
+    shard = StreamedShard(eng, parts, per, pxy, pgap, poll_s=poll_s, on_piece=on_piece)
+    return _exchange(shard, chunks, rank, P, device, group, final_status=True)
+
+
+def emulate_ranks(make_shard, world, chunks, P):
+    """Runs every rank's shard one after another in this process (one GPU
+    standing in for W) and exchanges the blocks by concatenation in rank
+    order -- exactly what all_gather_into_tensor returns -- then chains.
+    make_shard(rank) -> a started-able PipelinedShard / StreamedShard.
+    Returns (hash, penalties[P], hashes[P,64], per-rank per-piece ready times in s)."""
+    import time
+
+    blocks = [[None] * chunks for _ in range(world)]
+    ready = np.zeros((world, chunks))
+    for r in range(world):
+        sh = make_shard(r)
+        t0 = time.perf_counter()
+        sh.start()
+        for c in range(chunks):
+            blocks[r][c] = sh.block(c)
+            ready[r, c] = time.perf_counter() - t0
+        err = sh.finish()
+        if err is not None:
+            raise RankFailed("rank %d: %s" % (r, err)) from err
+    chain = seqalign.ChainStream(P)
+    try:
+        for c in range(chunks):
+            cid, cpen, chs = unpack_chunk(np.concatenate([blocks[r][c] for r in range(world)]))
+            chain.feed(cid, cpen, chs)
+        h, pen, hs = chain.finish()
+    finally:
+        chain.close()
+    return h, pen, hs, ready
 
 
 def align_sharded(align_fn, lengths, pxy, pgap, rank, world, device=None, group=None):
@@ -277,8 +359,7 @@ def align_sharded(align_fn, lengths, pxy, pgap, rank, world, device=None, group=
         rec = pack_records(ids, pen, hs, per)
     except Exception as e:  # still join the ONE collective, so no peer waits forever
         err = e
-        rec = pack_records([], [], [], per)
-        rec[:, :4] = np.array([FAILED], dtype=np.int32).view(np.uint8)
+        rec = failed_block(per)
     g = all_gather_records(rec, device=device, group=group)
     if err is not None:
         raise RankFailed("rank %d: %s" % (rank, err)) from err

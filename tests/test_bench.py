@@ -113,8 +113,11 @@ def test_bench_nccl_all_gather_at_world_one():
 
 @pytest.mark.gpu
 def test_two_ranks_streamed_records_big13_published_hash():
-    """dist.align_sharded_streamed: one launch per rank (band tasks, pair-major),
-    four pieces exchanged as their records arrive, rank 0 chaining each piece."""
+    """dist.align_sharded_streamed: one launch per rank (the engine's default
+    task order: largest pairs first, so records arrive in size order, not in
+    canonical order), four pieces each exchanged once all of its records have
+    arrived, rank 0 chaining each piece; the line records when each piece was
+    ready."""
     env = _env(NWK_BENCH_BACKEND="gloo", NWK_BENCH_SHARE_GPU="1", NWK_BENCH_WS_GB="110",
                      NWK_BENCH_STREAM="1", NWK_BENCH_CHUNKS="4")
     r = subprocess.run([sys.executable, "-u", BENCH, "--gpus", "2", "--workload", "big13",
@@ -124,3 +127,5 @@ def test_two_ranks_streamed_records_big13_published_hash():
     line = json.loads(r.stdout.decode().strip().split("\n")[-1])
     assert line["n_gpus"] == 2 and line["answer_hash_ok"] is True
     assert "streamed" in line["config"]["parallelism"]
+    ready = line["collective"]["piece_ready_ms"]
+    assert len(ready) == 4 and ready == sorted(ready)

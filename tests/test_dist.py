@@ -236,3 +236,131 @@ def test_gloo_pipelined_failing_piece_raises_everywhere():
     for r, msg in out.items():
         assert isinstance(msg, str) and msg.startswith("raised:"), (r, msg)
     assert "injected" in out[1]
+
+
+class _OracleStreamEngine(_OracleEngine):
+    """The streamed engine's begin / poll / end over the CPU oracle: poll
+    returns the records in order, a few pairs per call (test infrastructure).
+    fail_end: end() raises after every record has been polled -- the device
+    error word that only align_pairs_end reports."""
+
+    def __init__(self, genes, fail_end=False):
+        super().__init__(genes)
+        self.fail_end = fail_end
+
+    def align_pairs_begin(self, ids, pxy, pgap):
+        super().align_pairs_begin(ids, pxy, pgap)
+        self._pen, self._hs = _OracleEngine.align_pairs_end(self)  # computed up front, released by poll
+        self.ids, self._n = list(ids), 0
+
+    def align_pairs_poll(self, start=0):
+        self._n = min(len(self.ids), self._n + 3)
+        return self._n, self._pen[start:self._n].copy(), self._hs[start:self._n].copy()
+
+    def align_pairs_end(self):
+        self.ids = None
+        if self.fail_end:
+            raise RuntimeError("injected NWK_EKERNEL at align_pairs_end")
+        return self._pen, self._hs
+
+
+def _streamed_worker(rank, world, port, cases, chunks, fail, q):
+    import sys
+
+    for p in (PKG, ORACLE):
+        sys.path.insert(0, p)
+    import dist as nwdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        for name, pxy, pgap, genes in cases:
+            eng = _OracleStreamEngine(genes, fail_end=fail and rank == world - 1)
+            try:
+                h, pen, _ = nwdist.align_sharded_streamed(eng, [len(g) for g in genes], pxy, pgap, rank, world,
+                                                          chunks=chunks, poll_s=0.0)
+                q.put((rank, name, h, None if pen is None else [int(v) for v in pen]))
+            except nwdist.RankFailed as e:
+                q.put((rank, name, "raised: %s" % e, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 4)])
+def test_gloo_streamed_pieces_match_golden(world, chunks):
+    """dist.align_sharded_streamed (one launch per rank, records polled as they
+    stream, one all-gather per piece, final status collective): the answer
+    hash and penalties of the reference (golden) on rank 0."""
+    cases = []
+    for c in CASES:
+        pxy, pgap, genes = case_input(c)
+        cases.append((c["name"], pxy, pgap, genes))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_streamed_worker, args=(r, world, port, cases, chunks, False, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world * len(cases))]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    gold = {c["name"]: c for c in CASES}
+    for rank, name, h, pen in out:
+        if rank == 0:
+            assert h == gold[name]["hash"], name
+            assert pen == gold[name]["penalties"], name
+        else:
+            assert h is None
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_streamed_failure_at_end_raises_everywhere(world):
+    """The last rank's error surfaces only at align_pairs_end, after all of its
+    records were exchanged and chained by rank 0: the final status collective
+    makes every rank -- rank 0 included -- raise instead of returning a hash."""
+    genes = [b"ACGT" * 5, b"AC" * 7, b"GATTACA", b"T" * 11, b"CAT" * 4, b"GG" * 6, b"TACG" * 3]
+    cases = [("f", 3, 2, genes)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_streamed_worker, args=(r, world, port, cases, 3, True, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {r: h for r, _, h, _ in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r, msg in out.items():
+        assert isinstance(msg, str) and msg.startswith("raised:"), (r, msg)
+    assert "injected" in out[world - 1]
+
+
+def test_emulated_ranks_match_golden():
+    """dist.emulate_ranks (the one-GPU stand-in for W ranks that the full-size
+    GPU tests and tools/shardtime.py use): the same rank-side objects, the
+    all-gather replaced by concatenation in rank order."""
+    import sys
+
+    for p in (PKG, ORACLE):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import dist as nwdist
+
+    for c in CASES:
+        pxy, pgap, genes = case_input(c)
+        lengths = [len(g) for g in genes]
+        P = len(genes) * (len(genes) - 1) // 2
+        for world, chunks, streamed in ((2, 1, False), (3, 2, True), (4, 3, False)):
+            def make(r):
+                parts, per = nwdist.chunk_parts(lengths, r, world, chunks)
+                if streamed:
+                    return nwdist.StreamedShard(_OracleStreamEngine(genes), parts, per, pxy, pgap, poll_s=0.0)
+                return nwdist.PipelinedShard(_OracleEngine(genes), parts, per, pxy, pgap)
+
+            h, pen, _, ready = nwdist.emulate_ranks(make, world, chunks, P)
+            assert h == c["hash"], (c["name"], world, chunks)
+            assert [int(v) for v in pen] == c["penalties"]
+            assert ready.shape == (world, chunks)

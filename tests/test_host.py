@@ -83,6 +83,8 @@ def test_chain_stream_rejects_missing_and_duplicate_pairs():
         ch.feed([2], [0], hs[:1])  # fed twice
     with pytest.raises(seqalign.NwkError):
         ch.feed([4], [0], hs[:1])  # out of range
+    with pytest.raises(seqalign.NwkError):
+        ch.feed([1, 1], [0, 0], hs[:2])  # twice within one batch
     with pytest.raises(seqalign.NwkError) as e:
         ch.finish()  # pairs 1 and 3 never fed
     assert "never fed" in str(e.value)
