@@ -66,8 +66,9 @@ typedef struct nwk_opts {
                                 <= 4 symbols -- as 2048-row band tasks or, for jobs of many pairs per wave slot, as
                                 one rolling strip per pair, nw_align_strip), 1 nw_align, 2 nw_align_pk,
                                 3 nw_align_pk2, 4 nw_align_bits band tasks, 5 nw_align_strip wherever admissible
-                                (n / 64 in [63, 200] for pgap 2, [63, 500] for pgap 1; a kernel where it is not
-                                exact -- W > 4, mixed-sign K, pgap > 2 -- falls back) */
+                                (n / 64 in [63, 200] for pgap 2, [63, 500] for pgap 1), 6 nw_align_col (bit-parallel
+                                columns, nw_align_bits' domain; a kernel where it is not exact -- W > 4, mixed-sign K,
+                                pgap > 2 -- falls back) */
   int32_t collective;        /* nwk_get_minimum_penalties: 1 = take the sharded RCCL all-gather path even when
                                 ngpus == 1 (one communicator of one rank; tests the collective on a 1-GPU box) */
   int32_t task_order;        /* nw_align_bits band tasks: 0 auto (band-major above one round of wave slots), 1 pair-major

@@ -1,0 +1,654 @@
+// nwk_col.hip -- column-wise bit-parallel fill (mode kCol, kernel nw_align_col)
+// for the reference's linear-gap recurrence (skel:211-226, sub:478-487) with
+// pxy >= 0, pgap in {1, 2} and at most four distinct symbols: the domain of
+// nw_align_bits, with a pair's critical path cut from m + n anti-diagonal
+// steps to about n + m / 32.
+//
+// Recurrence down a column.  In G-space gaps cost 0, so down
+// column j the horizontal differences h(i) = G[i][j-1] - G[i][j] obey
+//     h(i) = max(e(i), h(i-1) - L(i)),   e(i) = max(S(i) - L(i), 0),
+// L(i) = v(i, j-1) the previous column's vertical difference and S = 2 pgap
+// (match) or 2 pgap - pxy (mismatch).  With thermometer planes t_k = [h > k]
+// (k < NP = 2 pgap) and l_d = [L > d] this is, level by level from the top,
+//     t_k(i) = G_k(i) | (P(i) & t_k(i-1)),   P = ~l_0,
+//     G_k = (match & ~l_{NP-1-k}) | ~l_{SR-1-k} | OR_{d>=1} (~l_d & t_{k+d}(i-1))
+// (SR = 2 pgap - pxy, ~l_{<0} = 0): a carry chain per level, resolved for 32
+// rows at once by one add -- A = P | G_k, B = G_k, S = A + B + cin gives the
+// carries c_i = G_i | (P_i & c_{i-1}) = t_k(i), and S ^ A ^ B = the carries
+// shifted up one row, exactly the planes U_k = t_k(i-1) = h(i-1, j) the rest
+// of the cell needs.  D = max(S, U, L) and v = D - U are nw_align_bits' plane
+// algebra; the stored traceback bits are the same (diag = match | D == S_mm,
+// up = [v == 0], skel:229-262's DIAG > UP > LEFT).
+//
+// Layout.  Bit b of lane t is row 32 t + b of a 2048-row band, and at step s
+// lane t works on column s - t: a column's 32-row words pass down the wave one
+// lane per step.  A lane's carry into its row 32 t comes from lane t - 1's
+// carry out of the previous step (same column): v_addc_co_u32 takes the carry
+// in and gives the carry out as 64-lane masks in SGPRs, so the hop to the next
+// lane is one scalar shift.  Lane 0 takes the band above's last row instead
+// (one bit per step from 32-column granules {epoch:32 | 32 plane bits}), and
+// lane 63's carries out are the band's last row for the band below, collected
+// by a scalar shift register and published per 32 columns.  A band therefore
+// trails the band above by ~96 steps instead of nw_align_bits' 2112, and a
+// pair's span is n + ~96 x bands steps.
+//
+// Stored layout per band: nw_align_bits' 8-step blocks (1024 dwords; diag
+// bits of step s, lane t at B * 1024 + ((s & 7) >> 2) * 256 + 4 t + (s & 3),
+// up bits 512 dwords further), here holding column s - t, rows 32 t .. + 31.
+// Windowed storage keeps bits_nblk blocks from bits_blk_lo(band) on: every
+// step with a cell within bits_w columns of the diagonal j = i n / m.
+#include "nwk_bits_dev.h"
+
+namespace nwk {
+namespace {
+
+// v_addc_co_u32 with the carry as a 64-lane SGPR mask: c in = lane t's carry
+// in, c out = lane t's carry out
+__device__ __forceinline__ unsigned col_addc(unsigned a, unsigned b, u64& c) {
+  unsigned s;
+  asm("v_addc_co_u32 %0, %1, %2, %3, %1" : "=v"(s), "+s"(c) : "v"(a), "v"(b));
+  // (an empty scalar asm on the carry: the optimizer would otherwise carry the
+  // asm's {vgpr, sgpr} result pair through loop phis, making the carry per-lane)
+  asm("" : "+s"(c));
+  return s;
+}
+
+// The carries' hop to the next lane, on the scalar unit (written out so the
+// compiler keeps it there): lane 63's carry out of the previous step (bit 63)
+// enters the band's last-row shift register acc, then c = (c << 1) | the band
+// above's bit QQ of this half (lane 0's carry in).
+template <int QQ>
+__device__ __forceinline__ void col_hop(u64& c, unsigned& acc, u64 inj) {
+  u64 t;
+  asm("s_bitcmp1_b64 %[c], 63\n\t"
+      "s_addc_u32 %[acc], %[acc], %[acc]\n\t"
+      "s_lshl_b64 %[c], %[c], 1\n\t"
+      "s_bfe_u64 %[t], %[inj], %[pos]\n\t"
+      "s_or_b64 %[c], %[c], %[t]"
+      : [c] "+s"(c), [acc] "+s"(acc), [t] "=&s"(t)
+      : [inj] "s"(inj), [pos] "i"(QQ | (1 << 16))
+      : "scc");
+}
+
+// G_K's middle terms OR_{d = D .. I-1} (~l_d & T_{K+d})
+template <int NP, int K, int D, int I>
+__device__ __forceinline__ unsigned col_mid(unsigned G, const unsigned (&l)[NP], const unsigned (&T)[NP]) {
+  if constexpr (D >= I) {
+    return G;
+  } else {
+    G = BOP3(G, l[D], T[K + D], kA | (~kB & kC));
+    return col_mid<NP, K, D + 1, I>(G, l, T);
+  }
+}
+
+// Level K: resolves t_K for this lane's 32 rows; T[K] = t_K shifted up one row
+// (bit 0 = the carry in), cout = this lane's carry out (t_K of its row 31)
+template <int NP, int SR, int K>
+__device__ __forceinline__ void col_level(unsigned match, unsigned P, const unsigned (&l)[NP], unsigned (&T)[NP],
+                                          u64& c) {
+  constexpr int J = SR - 1 - K;  // mismatch term ~l_J (none below 0)
+  constexpr int I = NP - 1 - K;  // match term ~l_I
+  unsigned G;
+  if constexpr (J >= I) {
+    G = ~l[J];  // ~l_I and every ~l_d with d <= I lie inside ~l_J
+  } else {
+    if constexpr (K == NP - 1) G = BOP3(match, l[0], l[0], kA & ~kB);  // match & ~l_0
+    else G = BOP3(l[I], match, T[NP - 1], ~kA & (kB | kC));           // ~l_I & (match | T_{NP-1})
+    constexpr int D0 = J + 1 > 1 ? J + 1 : 1;  // terms d <= J lie inside ~l_J
+    G = col_mid<NP, K, D0, I>(G, l, T);
+    if constexpr (J >= 0) G = BOP3(G, l[J], l[J], kA | ~kB);  // | ~l_J
+  }
+  if constexpr (J >= 0) {  // P = ~l_0 lies inside G: t_K = G, no carry chain
+    T[K] = col_addc(G, G, c);
+  } else {
+    const unsigned A = K == NP - 1 ? P : (P | G);  // (level NP-1: G inside P)
+    const unsigned S = col_addc(A, G, c);
+    T[K] = BOP3(S, A, G, kA ^ kB ^ kC);
+  }
+}
+
+template <int NP, int SR, int K>
+__device__ __forceinline__ void col_levels(unsigned match, unsigned P, const unsigned (&l)[NP], unsigned (&T)[NP],
+                                           u64 (&c)[NP]) {
+  col_level<NP, SR, K>(match, P, l, T, c[K]);
+  if constexpr (K > 0) col_levels<NP, SR, K - 1>(match, P, l, T, c);
+}
+
+template <int NP, int QQ, int K = 0>
+__device__ __forceinline__ void col_hops(u64 (&c)[NP], unsigned (&acc)[NP], const u64 (&inj)[NP]) {
+  col_hop<QQ>(c[K], acc[K], inj[K]);
+  if constexpr (K + 1 < NP) col_hops<NP, QQ, K + 1>(c, acc, inj);
+}
+
+// Eight steps s0 .. s0+7 (s0 % 8 == 0) of one band.
+//   x0, x1   code bit planes of this lane's 32 rows
+//   w0, w1   y window of this 32-step half (bit 31 - q = code of column s_half + q - lane)
+//   l        v planes of this lane's previous column
+//   c        per level: the carries out of the previous step (64-lane masks)
+//   acc      shift registers of lane 63's carries out (the band's last row)
+//   inj      the band above's last row for lane 0's columns of this half (bit q = column s_half + q)
+//   pub      CAP: acc after step s_half + 30's carries (columns s_half - 94 .. s_half - 63)
+//   MASK     steps of the first super-block: columns < 0 keep v = 0 (the left border)
+template <int NP, int SR, bool MASK, bool CAP, int BLK>
+__device__ __forceinline__ void col_block(int s0, int lane, unsigned x0, unsigned x1, unsigned w0, unsigned w1,
+                                          unsigned (&l)[NP], u64 (&c)[NP], unsigned (&acc)[NP],
+                                          const u64 (&inj)[NP], unsigned (&pub)[NP], unsigned* st, bool sto) {
+  unsigned dw[8], uw[8];
+  auto step = [&](auto qc) {
+    constexpr int q = decltype(qc)::value;
+    constexpr int qq = 8 * BLK + q;  // step s0 + q within its 32-step half
+    const int s = s0 + q;
+    const unsigned Y0 = (unsigned)((int)(w0 << qq) >> 31);  // code bits of column s - lane, as 0 / ~0
+    const unsigned Y1 = (unsigned)((int)(w1 << qq) >> 31);
+    const unsigned match = BOP3(x0 ^ Y0, x1, Y1, ~(kA | (kB ^ kC)));  // ~((x0^Y0) | (x1^Y1))
+    col_hops<NP, qq>(c, acc, inj);
+    if constexpr (CAP && q == 7) {
+#pragma unroll
+      for (int k = 0; k < NP; ++k) pub[k] = acc[k];
+    }
+    unsigned T[NP], D[NP], Vn[NP];
+    const unsigned P = ~l[0];
+    col_levels<NP, SR, NP - 1>(match, P, l, T, c);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) D[k] = k < SR ? ~0u : BOP3(match, T[k], l[k], kA | kB | kC);
+    bits_diffs<NP, SR>(T, D, Vn);  // v = D - U, U = T
+    if constexpr (MASK) {
+      const bool live = s >= lane;  // column s - lane >= 0
+#pragma unroll
+      for (int k = 0; k < NP; ++k) Vn[k] = live ? Vn[k] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) l[k] = Vn[k];
+    if constexpr (SR < 0) dw[q] = match;
+    else if constexpr (SR >= NP) dw[q] = ~0u;
+    else dw[q] = BOP3(match, D[SR], D[SR], kA | ~kB);  // match | ~D_SR
+    uw[q] = Vn[0];  // stored raw: UP is v == 0 (bit clear)
+    if constexpr ((q & 3) == 3) {
+      typedef unsigned u4 __attribute__((ext_vector_type(4)));
+      constexpr int h = q >> 2;
+      if (sto) {
+        __builtin_nontemporal_store(u4{dw[4 * h], dw[4 * h + 1], dw[4 * h + 2], dw[4 * h + 3]},
+                                    reinterpret_cast<u4*>(st + 256 * h));
+        __builtin_nontemporal_store(u4{uw[4 * h], uw[4 * h + 1], uw[4 * h + 2], uw[4 * h + 3]},
+                                    reinterpret_cast<u4*>(st + 512 + 256 * h));
+      }
+    }
+  };
+  step(std::integral_constant<int, 0>{});
+  step(std::integral_constant<int, 1>{});
+  step(std::integral_constant<int, 2>{});
+  step(std::integral_constant<int, 3>{});
+  step(std::integral_constant<int, 4>{});
+  step(std::integral_constant<int, 5>{});
+  step(std::integral_constant<int, 6>{});
+  step(std::integral_constant<int, 7>{});
+}
+
+// every active lane's p (a uniform result the compiler can see as one)
+__device__ __forceinline__ bool wall(bool p) { return __builtin_amdgcn_ballot_w64(!p) == 0ull; }
+
+// lane `sel`'s word of v := x (uniform x, sel)
+__device__ __forceinline__ unsigned writelane(unsigned v, int x, int sel) {
+  // (two scalar operands: the lane select goes through m0, the constant bus takes one SGPR)
+  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(v)
+               : "s"(__builtin_amdgcn_readfirstlane(x)), "s"(__builtin_amdgcn_readfirstlane(sel)) : "m0");
+  return v;
+}
+
+// s_ff1 of a uniform 64-bit mask (forced into SGPRs: a loop variable the
+// compiler keeps in VGPRs on some path would otherwise make the asm operand illegal)
+__device__ __forceinline__ int sff1u(u64 m) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)m), hi = __builtin_amdgcn_readfirstlane((unsigned)(m >> 32));
+  return sff1(((u64)hi << 32) | lo);
+}
+
+__device__ __forceinline__ int smax(int a, int b) {
+  int r;
+  asm("s_max_i32 %0, %1, %2" : "=s"(r) : "s"(__builtin_amdgcn_readfirstlane(a)), "s"(__builtin_amdgcn_readfirstlane(b)) : "scc");
+  return r;
+}
+
+// Traceback of one pair from (m, n) over the stored (diag, up) bits.
+//
+// Tiles are 64 columns (lane L holds column cts - L) by four row-lanes ta ..
+// ta - 3 (128 rows), eight dwords per lane: each lane loads its column's words
+// at steps column + row-lane.  A D move goes from (row r, lane L) to (r - 1,
+// L + 1), so every cell of a diagonal run has the same key K = r + L; a U move
+// stays in the lane (key K - 1), an L move goes to lane L + 1 (key K + 1).
+// Each lane re-indexes its column of bits by key once per tile (a funnel
+// shift), then the walk runs on the scalar unit: one ballot pair per new key
+// gives every lane's D and U bit on that key's diagonal; a D run stops at the
+// first lane >= L whose D bit is clear (s_ff1); a stop that moves U continues
+// down its lane's column (a vertical run read from that lane's key window by
+// v_readlane) until a cell moves D or L.  Per lane the moves are U^nU then one
+// D or L, written once per tile (prefix sum of the lanes' move counts) through
+// a 1 KB LDS ring flushed to ops[].  Storage bound: a cell is read only when
+// its column is >= the band's lowest stored step (then its step, column +
+// row-lane, is stored too); a walk that leaves flags the pair for a re-run
+// with full storage.
+__device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd, unsigned char* obuf, int lane,
+                                          unsigned* prog, int& o_len, int2& o_end, bool& o_out) {
+  const int nblk = pd.bits_nblk, win = pd.bits_w;
+  const int64_t bdw = (int64_t)nblk * 1024;  // dwords per band
+  const unsigned* mat = a.mat + pd.mat_off;
+  uint8_t* ops = a.ops + pd.ops_off;
+  const unsigned ob = (unsigned)(uintptr_t)obuf;
+  int Lc = 0, flushed = 0;
+  auto flush = [&](int upto) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int from = flushed & ~3;
+    for (int o = from + 4 * lane; o < upto; o += 256) {
+      unsigned v;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ob + (unsigned)(o & (kTraceRing - 1)))
+                   : "memory");
+      *reinterpret_cast<unsigned*>(ops + o) = v;
+    }
+    flushed = upto;
+  };
+  int b = (pd.m - 1) / kBR, r = (pd.m - 1) % kBR, c = pd.n - 1;
+  if (a.dbg_notrace) c = -1;  // NWK_NOTRACE (fill timing): no moves
+  int tb = -1, blo = 0, slo = 0;
+  bool bad = false, out = false;
+  // one tile ahead: anchored 64 columns on at the row-lane the walk is
+  // predicted to enter it (rows per column ~ m / n), 24 rows of slack above
+  unsigned nd[4] = {0, 0, 0, 0}, nu[4] = {0, 0, 0, 0};
+  int ncts = -1, nta = -1, nb_ = -1;
+  auto load_tile = [&](int bb, int blo_, int cts_, int ta_, unsigned (&d)[4], unsigned (&u)[4]) {
+    const int cl = cts_ - lane;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int t = ta_ - k < 0 ? 0 : ta_ - k;
+      int step = cl + t;
+      int rel = (step >> 3) - blo_;
+      const bool okl = cl >= 0 && (unsigned)rel < (unsigned)nblk;
+      step = okl ? step : 0;
+      rel = okl ? rel : 0;
+      const unsigned* p = mat + (int64_t)bb * bdw + (int64_t)rel * 1024 + ((step & 7) >> 2) * 256 + 4 * t + (step & 3);
+      d[k] = __builtin_nontemporal_load(p);
+      u[k] = __builtin_nontemporal_load(p + 512);
+    }
+  };
+  const int64_t rpc = ((int64_t)pd.m << 16) / pd.n;  // rows per column (16.16)
+  const u64 tc0 = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+  unsigned n_tiles = 0, n_dem = 0, n_stops = 0;
+  while (!out && c >= 0 && (b > 0 || r >= 0)) {
+    if (r < 0) {  // into the band above
+      --b;
+      r += kBR;
+    }
+    if (b != tb) {
+      blo = __builtin_amdgcn_readfirstlane(bits_blk_lo(b, pd.m, pd.n, win));
+      slo = 8 * blo;
+      tb = b;
+    }
+    const int ta = r >> 5;
+    {
+      const int step = c + ta;
+      if ((unsigned)((step >> 3) - blo) >= (unsigned)nblk || c < slo) {  // the path left the stored window
+        out = true;
+        break;
+      }
+    }
+    if (Lc - flushed >= kTraceRing - 256) flush(Lc & ~3);  // (a tile adds <= 64 + 128 moves)
+    const int rowlo = ta > 3 ? 32 * (ta - 3) : 0;
+    // the tile: the prefetched one when the walk entered it, else loaded now
+    int cts, tta;
+    unsigned vd[4], vu[4];
+    if (nb_ == b && c <= ncts && c > ncts - 32 && ta <= nta && ta >= nta - 2) {
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+      cts = ncts;
+      tta = nta;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        vd[k] = nd[k];
+        vu[k] = nu[k];
+      }
+    } else {
+      ++n_dem;
+      cts = c;
+      tta = ta;
+      load_tile(b, blo, cts, tta, vd, vu);
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    }
+    ++n_tiles;
+    const int trowlo = tta > 3 ? 32 * (tta - 3) : 0;
+    // prefetch the tile after this one
+    {
+      const int c2 = cts - 64;
+      const int rp = r - (int)(((int64_t)(cts - c + 64) * rpc) >> 16);
+      if (c2 >= slo && rp >= 24) {
+        nb_ = b;
+        ncts = c2;
+        int pa = (rp + 24) >> 5;
+        pa = pa > kBR / 32 - 1 ? kBR / 32 - 1 : pa;
+        nta = __builtin_amdgcn_readfirstlane(pa);
+        load_tile(b, blo, ncts, nta, nd, nu);
+      } else {
+        nb_ = -1;
+      }
+    }
+    (void)rowlo;
+    const int LL = smin(63, cts - slo);  // last lane whose column is >= the lowest stored step
+    int L = cts - c;
+    int K = r + L;
+    const int Kb = K - 16;
+    // key window: lane l's bit i = its cell at row Kb + i - l: bit q of the
+    // column {0, vd[3], vd[2], vd[1], vd[0], 0} (rows below / above the tile read 0)
+    unsigned WD, WU;
+    {
+      const int q = Kb - lane - 32 * (tta - 3) + 32;
+      const int dq = q >> 5, sh = q & 31;
+      const bool ok = q >= 0 && q < 160;
+      const unsigned dlo = dq == 1 ? vd[3] : dq == 2 ? vd[2] : dq == 3 ? vd[1] : dq == 4 ? vd[0] : 0u;
+      const unsigned dhi = dq == 0 ? vd[3] : dq == 1 ? vd[2] : dq == 2 ? vd[1] : dq == 3 ? vd[0] : 0u;
+      const unsigned ulo = dq == 1 ? vu[3] : dq == 2 ? vu[2] : dq == 3 ? vu[1] : dq == 4 ? vu[0] : ~0u;
+      const unsigned uhi = dq == 0 ? vu[3] : dq == 1 ? vu[2] : dq == 2 ? vu[1] : dq == 3 ? vu[0] : ~0u;
+      WD = ok ? __builtin_amdgcn_alignbit(dhi, dlo, sh) : 0u;
+      WU = ok ? __builtin_amdgcn_alignbit(uhi, ulo, sh) : ~0u;  // stored up word: 0 = UP
+    }
+    const int L0 = L;
+    u64 finL = 0;          // lanes whose last move is L
+    unsigned nUv = 0;      // per lane: U moves (written by v_writelane)
+    int maxU = 0;
+    int Kc = -(1 << 30);
+    u64 Dm = 0, Um = 0;
+    for (;;) {
+      const int bnd = smin(K - trowlo, LL);
+      if (L > bnd) break;  // the cell is below the tile's rows or past its columns
+      const int i = K - Kb;
+      if ((unsigned)i > 31u) break;  // off the key window: a new tile here
+      if (K != Kc) {
+        Dm = __builtin_amdgcn_ballot_w64((WD >> i) & 1u);
+        Um = __builtin_amdgcn_ballot_w64(!((WU >> i) & 1u));
+        Kc = K;
+      }
+      const int lend = bnd + 1;  // first lane past the readable cells of this key
+      const u64 stops = ~Dm & (~0ull << L);
+      const int ls = sminu(sff1u(stops), lend);  // (no stop: ff1 = -1)
+      if (ls >= lend) {  // D moves through lanes L .. lend - 1
+        L = lend;
+        break;
+      }
+      ++n_stops;
+      if ((Um >> ls) & 1ull) {
+        // a U move, then down lane ls's column: U while D is clear and U set
+        const unsigned wd = (unsigned)__builtin_amdgcn_readlane((int)WD, ls);
+        const unsigned wu = (unsigned)__builtin_amdgcn_readlane((int)WU, ls);
+        const int jlo = smax(trowlo + ls - Kb, 0);  // lowest key bit inside the tile's rows
+        const unsigned below = i >= 31 ? ~0u : ((2u << i) - 1u);
+        const unsigned stopm = (wd | wu) & below & ~((1u << jlo) - 1u);
+        if (stopm == 0u) {  // the run leaves the tile's rows (or the key window): U moves down to there
+          const int nU = i - jlo + 1;
+          nUv = writelane(nUv, nU, ls);
+          maxU = nU > maxU ? nU : maxU;
+          L = ls;
+          K = Kb + jlo - 1;
+          break;
+        }
+        const int j = 31 - __builtin_clz(stopm);
+        const int nU = i - j;
+        nUv = writelane(nUv, nU, ls);
+        maxU = nU > maxU ? nU : maxU;
+        if ((wd >> j) & 1u) {  // the cell at key j moves D
+          K = Kb + j;
+        } else {  // ... or L
+          finL |= 1ull << ls;
+          K = Kb + j + 1;
+        }
+        L = ls + 1;
+      } else {  // an L move
+        finL |= 1ull << ls;
+        L = ls + 1;
+        K = K + 1;
+      }
+    }
+    // the tile's moves in walk order: lanes L0 .. L - 1 are done (U^nU, then D
+    // or L), lane L (when <= 63) holds only its U moves so far
+    {
+      const bool vis = lane >= L0 && lane <= L;
+      const bool fin = lane >= L0 && lane < L;
+      const unsigned nU = vis ? nUv : 0u;
+      const unsigned cnt = nU + (fin ? 1u : 0u);
+      const unsigned inc = shadev::wave_incl_scan(cnt, lane);
+      const unsigned off = inc - cnt;
+      const unsigned tot = (unsigned)__builtin_amdgcn_readlane((int)inc, 63);
+      for (int j = 0; j < maxU; ++j)
+        if ((unsigned)j < nU)
+          asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((Lc + (int)off + j) & (kTraceRing - 1))), "v"((unsigned)'U')
+                       : "memory");
+      if (fin) {
+        const unsigned ch = ((finL >> lane) & 1ull) ? 'L' : 'D';
+        asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((Lc + (int)(off + nU)) & (kTraceRing - 1))), "v"(ch)
+                     : "memory");
+      }
+      Lc += (int)tot;
+    }
+    r = K - L;
+    c = cts - L;
+    if (Lc > pd.m + pd.n) {
+      bad = true;
+      break;
+    }
+  }
+  if (bad && lane == 0) atomicOr(a.err, 16u);
+  if (a.stamps && lane == 0) {
+    u64* x = a.stamps + 8 * pd.slot;
+    x[2] = __builtin_amdgcn_s_memtime() - tc0;
+    x[3] = n_stops;
+    x[4] = (u64)Lc;
+    x[5] = ((u64)n_tiles << 32) | ((u64)n_dem << 16);
+  }
+  flush(Lc);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  o_len = out ? 0 : Lc;
+  o_end = (a.dbg_notrace || out) ? make_int2(pd.m, pd.n) : make_int2(b * kBR + r + 1, c + 1);
+  o_out = out;
+  if (lane == 0) {
+    a.oplen[pd.slot] = o_len;
+    a.endij[pd.slot] = o_end;
+    if (out) a.retry[pd.slot] = 1;
+  }
+  (void)prog;
+}
+
+// FUSE: the instantiation with the fused finalize (FillArgs::fuse_fin)
+template <int NP, int SR, bool FUSE>
+__global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_col(FillArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned char obuf_all[4][kTraceRing];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  unsigned* prog = a.prog ? a.prog + blockIdx.x * 4 + wid : nullptr;  // NWK_WATCHDOG markers
+
+  for (;;) {
+    if constexpr (FUSE) {  // queued pairs to hash: whole groups between fill tasks
+      while (hq_hash(a, lane, false)) {
+      }
+    }
+    unsigned tk = 0;
+    if (lane == 0) tk = atomicAdd(a.counter, 1u);
+    tk = __builtin_amdgcn_readfirstlane(tk);
+    BITS_PROG(0x10000000u | tk);
+    if (tk >= (unsigned)a.ntasks) {
+      if constexpr (FUSE) hq_drain(a, lane);
+      BITS_PROG(0x60000000u);
+      return;
+    }
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)a.err, BITS_RLX)) != 0u) return;
+    const int2 task = a.tasks[tk];
+    const PairDesc pd = a.pairs[task.x];
+    const int band = task.y;
+    const int R0 = band * kBR;
+    // code bit planes of rows R0 + 32 lane + b (rows past m: code 0, never traced)
+    unsigned x0 = 0, x1 = 0;
+    {
+      const int base = R0 + 32 * lane;
+      const int nv = pd.m - base;
+      const uint8_t* xc = a.codes + pd.x_off + base;
+#pragma unroll
+      for (int b = 0; b < 32; ++b) {
+        const unsigned cd = b < nv ? (unsigned)xc[b] : 0u;
+        x0 |= (cd & 1u) << b;
+        x1 |= ((cd >> 1) & 1u) << b;
+      }
+    }
+    unsigned l[NP], acc[NP], pub[NP];
+    u64 c[NP], inj[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      l[k] = acc[k] = pub[k] = 0u;
+      c[k] = inj[k] = 0ull;
+    }
+    const bool from_above = band > 0;
+    const bool to_below = band + 1 < pd.nbands;
+    const int nw = (pd.n + 31) >> 5;  // 32-column words of a row
+    const int nsb = pd.sblocks;
+    const u64* gin = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)(from_above ? band - 1 : 0) * nw * NP;
+    u64* gout = a.bnd + pd.bnd_off + (int64_t)band * nw * NP;
+    const int nblk = pd.bits_nblk, blo = bits_blk_lo(band, pd.m, pd.n, pd.bits_w);
+    unsigned* mb = a.mat + pd.mat_off + (int64_t)band * nblk * 1024 + lane * 4;
+    // y windows: lane t's window for the half starting at step s_h is position s_h - t
+    const unsigned* ywp = a.yw + 2 * (pd.e_off - (int64_t)lane);
+    unsigned wc0 = ywp[0], wc1 = ywp[1];
+    // granule k of a 32-column word is polled by lane k; every lane loads one
+    // (lanes >= NP a copy) so no branch depends on the lane: a lane-dependent
+    // branch here would make the compiler treat the carries as per-lane values
+    const bool gl = lane < NP;
+    const int gk = lane & (NP - 1);
+    u64 g = 0;
+    if (from_above) g = __hip_atomic_load((gu64*)(gin + gk), BITS_RLX);
+    bool ok = true;
+
+    auto half = [&](int h, auto mask_t) {
+      constexpr bool MASK = decltype(mask_t)::value;
+      const unsigned* wp = ywp + 64 * (h + 1);
+      const unsigned nx0 = wp[0], nx1 = wp[1];  // the next half's window
+      if (from_above) {
+        if (h < nw) {
+          if (!wall(!gl || (unsigned)(g >> 32) == a.epoch)) {
+            g = bits_wait(gin + (int64_t)h * NP + gk, gl, a.epoch, g, a.err);
+            // (a failed wait ends the task after this half, which publishes nothing; the
+            // error word fails the call.  No early return: it would leave the carries
+            // undefined on one path, and the compiler then moves them out of SGPRs)
+            if (!wall(!gl || (unsigned)(g >> 32) == a.epoch)) ok = false;
+          }
+          const unsigned dat = (unsigned)g;
+#pragma unroll
+          for (int k = 0; k < NP; ++k) inj[k] = (u64)(unsigned)__builtin_amdgcn_readlane((int)dat, k);
+          if (h + 1 < nw) g = __hip_atomic_load((gu64*)(gin + (int64_t)(h + 1) * NP + gk), BITS_RLX);
+        } else {
+#pragma unroll
+          for (int k = 0; k < NP; ++k) inj[k] = 0ull;
+        }
+      }
+      auto blk = [&](auto bc) {
+        constexpr int B = decltype(bc)::value;
+        const int s0 = 32 * h + 8 * B;
+        const int rel = (s0 >> 3) - blo;
+        const bool sto = (unsigned)rel < (unsigned)nblk;
+        unsigned* st = mb + (int64_t)rel * 1024;
+        col_block<NP, SR, MASK, B == 3, B>(s0, lane, x0, x1, wc0, wc1, l, c, acc, inj, pub, st, sto);
+      };
+      blk(std::integral_constant<int, 0>{});
+      blk(std::integral_constant<int, 1>{});
+      blk(std::integral_constant<int, 2>{});
+      blk(std::integral_constant<int, 3>{});
+      // publish the band's last row, columns 32 (h - 2) .. + 31 (lane 63's carries of steps 32 h - 1 .. 32 h + 30,
+      // MSB first in pub)
+      if (to_below && ok && h >= 2 && h - 2 < nw) {
+        unsigned v = 0;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) v = gk == k ? __builtin_bitreverse32(pub[k]) : v;
+        // (every lane stores: lanes >= NP repeat lane gk's granule, so no branch depends on the lane)
+        __hip_atomic_store((gu64*)(gout + (int64_t)(h - 2) * NP + gk), ((u64)a.epoch << 32) | v, BITS_RLX);
+      }
+      wc0 = nx0;
+      wc1 = nx1;
+    };
+    // the first super-block (columns < 0 masked) peeled off the loop
+    half(0, std::true_type{});
+    half(1, std::true_type{});
+    for (int sb = 1; sb < nsb && ok; ++sb) {
+      half(2 * sb, std::false_type{});
+      half(2 * sb + 1, std::false_type{});
+    }
+    BITS_PROG(0x30000000u);
+    if (!ok) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add((gu32*)(a.done + pd.slot), 1u, BITS_RLX);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev + 1u == (unsigned)pd.nbands) {  // the pair's last band: every band has released
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      BITS_PROG(0x40000000u);
+      if (a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
+      int tlen;
+      int2 tend;
+      bool tout;
+      trace_col(a, pd, obuf_all[wid], lane, prog, tlen, tend, tout);
+      if constexpr (FUSE) {
+        const bool ok_rows = !tout && fin_rows(a, pd, lane, tlen, tend);
+        hq_push(a, pd, lane, ok_rows);
+      }
+      if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
+      BITS_PROG(0x56000000u);
+    }
+  }
+}
+
+template <int NP, int SR>
+hipError_t col_launch(const FillArgs& a, int grid, hipStream_t s) {
+#ifdef NWK_COL_NOFUSE
+  if (a.fuse_fin) return hipErrorInvalidValue;
+#else
+  if (a.fuse_fin) hipLaunchKernelGGL((nw_align_col<NP, SR, true>), dim3(grid), dim3(256), 0, s, a);
+  else
+#endif
+  hipLaunchKernelGGL((nw_align_col<NP, SR, false>), dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int NP, int SR>
+int col_occ() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&nw_align_col<NP, SR, false>), 256, 0) !=
+      hipSuccess)
+    return 1;
+  return n > 0 ? n : 1;
+}
+
+}  // namespace
+
+int bits_sr(int pxy, int pgap);
+
+hipError_t launch_col(const FillArgs& a, int pxy, int pgap, int grid, hipStream_t s) {
+  const int sr = bits_sr(pxy, pgap);
+#ifdef NWK_COL_ONE  // (development: one instantiation, fast builds)
+  return pgap == 2 && sr == 1 ? col_launch<4, 1>(a, grid, s) : hipErrorInvalidValue;
+#endif
+  if (pgap == 1) {
+    switch (sr) {
+      case -1: return col_launch<2, -1>(a, grid, s);
+      case 0: return col_launch<2, 0>(a, grid, s);
+      case 1: return col_launch<2, 1>(a, grid, s);
+      default: return col_launch<2, 2>(a, grid, s);
+    }
+  }
+  if (pgap == 2) {
+    switch (sr) {
+      case -1: return col_launch<4, -1>(a, grid, s);
+      case 0: return col_launch<4, 0>(a, grid, s);
+      case 1: return col_launch<4, 1>(a, grid, s);
+      case 2: return col_launch<4, 2>(a, grid, s);
+      case 3: return col_launch<4, 3>(a, grid, s);
+      default: return col_launch<4, 4>(a, grid, s);
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+int col_blocks_per_cu(int pgap) { return pgap == 1 ? col_occ<2, 1>() : col_occ<4, 1>(); }
+
+}  // namespace nwk

@@ -28,6 +28,7 @@ enum Mode : int {
   kAffinePk = 7,   // kAffine on band pairs as int16 pairs (nw_align_pka), layout LY 2, profile codes
   kBits = 8,       // bit-sliced difference planes (nw_align_bits, nwk_bits.hip): 2048-row bands, 2-bit traceback
   kBitsStrip = 9,  // kBits as rolling strips (nw_align_strip): one wave per pair, every band in turn
+  kCol = 10,       // bit-parallel columns (nw_align_col, nwk_col.hip): kBits' domain and storage, a pair's span n + ~96 x bands
 };
 constexpr int kBitsRows = 2048;  // kBits: rows per band (64 lanes x 32 bits)
 
@@ -186,6 +187,9 @@ hipError_t launch_bits(const FillArgs& a, int pxy, int pgap, int grid, hipStream
 int bits_blocks_per_cu(int pgap);
 hipError_t launch_strip(const FillArgs& a, int pxy, int pgap, int grid, hipStream_t s);
 int strip_blocks_per_cu(int pgap, int ring_dwords);
+// kCol (nwk_col.hip)
+hipError_t launch_col(const FillArgs& a, int pxy, int pgap, int grid, hipStream_t s);
+int col_blocks_per_cu(int pgap);
 
 // Dwords of one band of the stored matrix.
 __host__ __device__ inline int64_t band_dwords(int bits, int sblocks) {

@@ -493,8 +493,12 @@ int choose_plan(const nwk_ctx* c, const Scoring& sc, Plan* pl) {
   // driver's NWK_BITS is the storage width, opts.bits).
   // pl->bits keeps the profile kernels' width (the linear-space path uses it).
   static const int bits_env = getenv("NWK_BITS_KERNEL") ? atoi(getenv("NWK_BITS_KERNEL")) : 1;
-  const bool want_bits = c->opts.kernel == 4 || c->opts.kernel == 5 || (c->opts.kernel == 0 && bits_env != 0);
+  const bool want_bits = c->opts.kernel == 4 || c->opts.kernel == 5 || c->opts.kernel == 6 ||
+                         (c->opts.kernel == 0 && bits_env != 0);
   if (want_bits && c->opts.bits == 0 && bits_admissible(pxy, pgap, c->alpha)) pl->mode = kBits;
+  // bit-parallel columns (nw_align_col, same domain): opts.kernel 6, or NWK_COL=1 under "auto"
+  static const int col_env = getenv("NWK_COL") ? atoi(getenv("NWK_COL")) : 0;
+  if (pl->mode == kBits && (c->opts.kernel == 6 || (c->opts.kernel == 0 && col_env == 1))) pl->mode = kCol;
   return NWK_OK;
 }
 
@@ -535,6 +539,20 @@ int64_t bits_nblk_of(int m, int n, int w) {
   const int64_t all = 8 * (int64_t)bits_sblocks(ceil_div(n, 64));
   if (w <= 0) return all;
   const int64_t width = (kBitsRows - 1) + ceil_div((int64_t)(kBitsRows - 1) * n, m) + 2 * (int64_t)w + 16;
+  return std::min(all, ceil_div(width, 8) + 1);
+}
+
+// kCol geometry (nw_align_col, nwk_col.hip): lane t works on column s - t at
+// step s; a band runs until lane 63 has column n - 1 and its last 32-column
+// word of the band's last row is published (step 32 ceil(n / 32) + 94):
+// 64 * (nchunks + 2) steps.  Stored blocks per band: every block, or (bits_w
+// > 0) from bits_blk_lo(b) = (b 2048 n / m - w) / 8 on, covering every step
+// c + t with |c - i n / m| <= w over the band's rows i (t < 64).
+inline int col_sblocks(int64_t nch) { return (int)(nch + 2); }
+int64_t col_nblk_of(int m, int n, int w) {
+  const int64_t all = 8 * (int64_t)col_sblocks(ceil_div(n, 64));
+  if (w <= 0) return all;
+  const int64_t width = ceil_div((int64_t)(kBitsRows - 1) * n, m) + 2 * (int64_t)w + 64 + 16;
   return std::min(all, ceil_div(width, 8) + 1);
 }
 
@@ -616,6 +634,16 @@ void footprint(PairWork* w, int bits, int mode, bool affine) {
     // layout) are written on one XCD and hashed on another, so no line may be
     // shared with a neighbour's rows (a stale copy in the hashing XCD's L2)
     w->ops_b = round_up((int64_t)w->m + w->n, 128);
+    return;
+  }
+  if (mode == kCol) {
+    const int64_t nb = ceil_div(w->m, kBitsRows), nw = ceil_div(w->n, 32);
+    w->segops_b = w->segctl_b = 0;
+    w->spec = 0;
+    w->bits_nblk = (int)col_nblk_of(w->m, w->n, w->bits_w);
+    w->mat_dw = nb * w->bits_nblk * 1024;
+    w->bnd_gr = (nb - 1) * nw * 4;  // NP <= 4 granules per 32 columns of each band's last row
+    w->ops_b = round_up((int64_t)w->m + w->n, 128);  // (whole lines per pair: the fused finalize's rows)
     return;
   }
   if (mode == kBits) {
@@ -807,7 +835,7 @@ LinGeo lin_geo(const Plan& pl, const PairWork& w, int G) {
 
 Plan lin_plan(const Plan& pl0) {
   Plan pl = pl0;
-  if (pl.mode == kPacked || pl.mode == kPacked2 || pl.mode == kBits || pl.mode == kBitsStrip)
+  if (pl.mode == kPacked || pl.mode == kPacked2 || pl.mode == kBits || pl.mode == kBitsStrip || pl.mode == kCol)
     pl.mode = kProfile;  // same bits, codes, K0/K1
   return pl;
 }
@@ -1058,7 +1086,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     const int want = c->opts.kernel == 5 ? 1 : c->opts.kernel == 4 ? 0 : strip_env;
     if (want != 0 && use_strips(c, work, sc.pgap, want == 1, &strip_ring)) pl.mode = kBitsStrip;
   }
-  const bool bitsy = pl.mode == kBits || pl.mode == kBitsStrip;
+  const bool bitsy = pl.mode == kBits || pl.mode == kBitsStrip || pl.mode == kCol;
   st.bits = bitsy ? 2 : pl.bits;
   st.mode = pl.mode;
   int rc;
@@ -1175,6 +1203,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     }
   }
   int bpc = pl.mode == kBits        ? bits_blocks_per_cu(sc.pgap)
+            : pl.mode == kCol       ? col_blocks_per_cu(sc.pgap)
             : pl.mode == kBitsStrip ? strip_blocks_per_cu(sc.pgap, strip_ring)
                                     : fill_blocks_per_cu(pl.mode, pl.bits);
   // waves per SIMD: nw_align_pk2 measured best at 2 (band chains run at the
@@ -1318,6 +1347,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       d.nbands = (int)ceil_div(w.m, bitsy ? kBitsRows : kBandRows);
       d.nchunks = pl.mode == kBitsStrip ? d.bits_np / 64 : (int)ceil_div(w.n, 64);
       d.sblocks = pl.mode == kBits        ? bits_sblocks(d.nchunks)
+                  : pl.mode == kCol       ? col_sblocks(d.nchunks)
                   : pl.mode == kBitsStrip ? strip_sblocks(w.m, w.n)
                                           : sblocks_of(pl.mode, d.nchunks);
       d.bits_w = w.bits_w;
@@ -1355,6 +1385,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     if (order < 0 && pl.mode == kBits && c->opts.task_order > 0) order = c->opts.task_order == 1 ? 0 : 1;
     if (order < 0) order = (pl.mode == kBits || pl.mode == kAffinePk) && ntasks > 4 * (int64_t)grid ? 1 : 0;
     if (pl.mode == kBitsStrip) order = 0;  // one task per pair, largest first
+    // kCol: bands trail each other by ~96 steps, so a pair's bands dequeued
+    // together run as one short pipeline: pair-major unless NWK_ORDER says otherwise
+    if (pl.mode == kCol && order_env < 0) order = c->opts.task_order == 2 ? 1 : 0;
     if (order == 1) {  // band-major (experiment)
       for (int b = 0; b < maxb; ++b)
         for (int q = 0; q < np; ++q)
@@ -1504,6 +1537,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     if (pl.mode == kBits)
       HIP_TRY(launch_bits(fa, sc.pxy, sc.pgap, (int)std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
+    else if (pl.mode == kCol)
+      HIP_TRY(launch_col(fa, sc.pxy, sc.pgap, (int)std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     else if (pl.mode == kBitsStrip)
       HIP_TRY(launch_strip(fa, sc.pxy, sc.pgap, (int)std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     else

@@ -24,10 +24,10 @@ LIB_PATH = os.path.join(HERE, "lib", "libnwk.so")
 NWK_OK = 0
 ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "EKERNEL", -5: "ECOMM"}
 MODES = {0: "profile", 1: "compare", 2: "literal", 3: "affine", 4: "packed-profile", 5: "packed-band-pairs",
-         7: "packed-affine-band-pairs", 8: "bit-sliced-planes", 9: "bit-sliced-strips"}
+         7: "packed-affine-band-pairs", 8: "bit-sliced-planes", 9: "bit-sliced-strips", 10: "bit-parallel-columns"}
 # fill kernel of each mode (csrc/nwk_kernels.hip), as rocprofv3 names it
 KERNELS = {0: "nw_align", 1: "nw_align", 2: "nw_align", 3: "nw_align_affine", 4: "nw_align_pk", 5: "nw_align_pk2",
-           7: "nw_align_pka", 8: "nw_align_bits", 9: "nw_align_strip"}
+           7: "nw_align_pka", 8: "nw_align_bits", 9: "nw_align_strip", 10: "nw_align_col"}
 
 
 class NwkError(RuntimeError):
@@ -94,8 +94,12 @@ _lib = None
 # per-launch counters (profiles/<round>/pmc_<workload>.json) can be tied to the
 # kernel build that produced them.
 KERNEL_SOURCES = {
-    "nw_align_bits": ("csrc/nwk_bits.hip", "csrc/nwk_sha_dev.h", "csrc/nwk_internal.h", "Makefile"),
-    "nw_align_strip": ("csrc/nwk_bits.hip", "csrc/nwk_sha_dev.h", "csrc/nwk_internal.h", "Makefile"),
+    "nw_align_bits": ("csrc/nwk_bits.hip", "csrc/nwk_bits_dev.h", "csrc/nwk_sha_dev.h", "csrc/nwk_internal.h",
+                      "Makefile"),
+    "nw_align_strip": ("csrc/nwk_bits.hip", "csrc/nwk_bits_dev.h", "csrc/nwk_sha_dev.h", "csrc/nwk_internal.h",
+                       "Makefile"),
+    "nw_align_col": ("csrc/nwk_col.hip", "csrc/nwk_bits_dev.h", "csrc/nwk_sha_dev.h", "csrc/nwk_internal.h",
+                     "Makefile"),
     "nw_align_pka": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
     "nw_align_pk2": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
     "nw_align_pk": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
@@ -181,7 +185,8 @@ class Engine:
 
     FINALIZE = {"auto": 0, "host": 1, "device": 2, "fused": 3}
 
-    KERNEL = {"auto": 0, "nw_align": 1, "nw_align_pk": 2, "nw_align_pk2": 3, "nw_align_bits": 4, "nw_align_strip": 5}
+    KERNEL = {"auto": 0, "nw_align": 1, "nw_align_pk": 2, "nw_align_pk2": 3, "nw_align_bits": 4, "nw_align_strip": 5,
+              "nw_align_col": 6}
 
     def __init__(self, device=0, bits=0, workspace_bytes=0, host_threads=0, verbose=False, finalize="auto",
                  linear_space=0, kernel="auto", task_order=0):
