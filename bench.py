@@ -345,6 +345,8 @@ def main():
     ap.add_argument("--bits", type=int, default=0, help="force DP storage width (4/8/16/32)")
     ap.add_argument("--affine", default=None,
                     help="go,ge: run the affine-gap variant (default for --workload c5: 3,1)")
+    ap.add_argument("--kernel", default="auto",
+                    help="linear fill kernel (seqalign.Engine.KERNEL): auto, nw_align_bits, nw_align_col, ...")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
@@ -407,7 +409,7 @@ def main():
     # chained as they complete (C4 at 8 ranks: 24.3 ms vs 28.4 ms)
     stream = sharded and not affine and int(os.environ.get("NWK_BENCH_STREAM", "1" if P >= 8192 else "0")) == 1
     eng = seqalign.Engine(device=gpu, bits=args.bits, verbose=args.verbose, workspace_bytes=ws,
-                          finalize="fused" if stream else "auto")
+                          finalize="fused" if stream else "auto", kernel=args.kernel)
     eng.set_sequences(genes)  # sequences resident in HBM before timing
     my_ids = seqalign.shard_pairs(lengths, rank, world) if sharded else np.arange(P, dtype=np.int64)
 

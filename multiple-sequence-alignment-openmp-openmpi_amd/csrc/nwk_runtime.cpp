@@ -251,7 +251,7 @@ int nwk_ctx_create(const nwk_opts* opts, nwk_ctx** out) {
   if (const char* v = getenv("NWK_VERBOSE")) o.verbose = atoi(v);  // debug: diagnostics on stderr
   // option checks first: they need no device
   if (o.finalize < 0 || o.finalize > 3) return fail(NWK_EINVAL, "nwk_ctx_create: finalize must be 0..3");
-  if (o.kernel < 0 || o.kernel > 5) return fail(NWK_EINVAL, "nwk_ctx_create: kernel must be 0..5");
+  if (o.kernel < 0 || o.kernel > 6) return fail(NWK_EINVAL, "nwk_ctx_create: kernel must be 0..6");
   if (o.task_order < 0 || o.task_order > 2) return fail(NWK_EINVAL, "nwk_ctx_create: task_order must be 0..2");
   if (o.bits != 0 && o.bits != 4 && o.bits != 8 && o.bits != 16 && o.bits != 32)
     return fail(NWK_EINVAL, "nwk_ctx_create: bits must be 0/4/8/16/32");

@@ -60,7 +60,8 @@ def check(h, pen, what):
         sys.exit("shardtime: %s: the gathered answer differs from %s" % (what, gold.get("source", "the golden")))
 
 
-e = seqalign.Engine(device=0)
+KERNEL = os.environ.get("NWK_ST_KERNEL", "auto")  # e.g. nw_align_col
+e = seqalign.Engine(device=0, kernel=KERNEL)
 e.set_sequences(g)
 e.align_pairs(np.arange(P, dtype=np.int64), pxy, pgap)  # warm
 
@@ -88,7 +89,7 @@ for W in [int(a) for a in args] or [1, 2, 4, 8]:
         continue
     if stream and es is None:  # records fused into the fill launch (dist.StreamedShard)
         e.close()  # (its workspace holds most of the HBM)
-        es = seqalign.Engine(device=0, finalize="fused", kernel=os.environ.get("NWK_ST_KERNEL", "auto"),
+        es = seqalign.Engine(device=0, finalize="fused", kernel=KERNEL,
                              task_order=int(os.environ.get("NWK_ST_ORDER", "0")))
         es.set_sequences(g)
         es.align_pairs(np.arange(min(P, 64), dtype=np.int64), pxy, pgap)
