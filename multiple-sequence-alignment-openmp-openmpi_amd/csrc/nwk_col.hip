@@ -202,6 +202,13 @@ __device__ __forceinline__ int sff1u(u64 m) {
   return sff1(((u64)hi << 32) | lo);
 }
 
+// windowed storage: a lane's words of an 8-step block (dev = c m - i n over
+// them spans [hi - 7 m - 31 n, hi]) are stored iff that span meets
+// [-lim, lim], lim = bits_w m; hlim = lim + 7 m + 31 n
+__device__ __forceinline__ bool bits_lane_stored(int64_t hi, int64_t lim, int64_t hlim) {
+  return hi >= -lim && hi <= hlim;
+}
+
 __device__ __forceinline__ int smax(int a, int b) {
   int r;
   asm("s_max_i32 %0, %1, %2" : "=s"(r) : "s"(__builtin_amdgcn_readfirstlane(a)), "s"(__builtin_amdgcn_readfirstlane(b)) : "scc");
@@ -248,6 +255,11 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
   int b = (pd.m - 1) / kBR, r = (pd.m - 1) % kBR, c = pd.n - 1;
   if (a.dbg_notrace) c = -1;  // NWK_NOTRACE (fill timing): no moves
   int tb = -1, blo = 0, slo = 0;
+  const int64_t lim = (int64_t)win * pd.m;
+  if (win > 0 && c >= 0) {  // the walk's first cell
+    const int64_t dev = (int64_t)c * pd.m - (int64_t)(pd.m - 1) * pd.n;
+    if (dev > lim || dev < -lim) c = -2;  // (out below)
+  }
   bool bad = false, out = false;
   // one tile ahead: anchored 64 columns on at the row-lane the walk is
   // predicted to enter it (rows per column ~ m / n), 24 rows of slack above
@@ -271,6 +283,7 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
   const int64_t rpc = ((int64_t)pd.m << 16) / pd.n;  // rows per column (16.16)
   const u64 tc0 = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
   unsigned n_tiles = 0, n_dem = 0, n_stops = 0;
+  if (c == -2) out = true;
   while (!out && c >= 0 && (b > 0 || r >= 0)) {
     if (r < 0) {  // into the band above
       --b;
@@ -331,6 +344,17 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
     const int LL = smin(63, cts - slo);  // last lane whose column is >= the lowest stored step
     int L = cts - c;
     int K = r + L;
+    // windowed storage keeps only the lane words holding a cell within bits_w
+    // columns of the diagonal: a cell read must have |dev| <= lim, dev = c m - i n.
+    // Tiles wholly inside skip the checks; near the window's edge each run's end
+    // cells are checked (dev is linear along a D or U run)
+    const int64_t ib = (int64_t)b * kBR;
+    const bool wchk = win > 0 && ((int64_t)cts * pd.m - (ib + trowlo) * pd.n > lim ||
+                                  (int64_t)(cts - 63) * pd.m - (ib + trowlo + 127) * pd.n < -lim);
+    auto outside = [&](int Ll, int Kk) {
+      const int64_t dev = (int64_t)(cts - Ll) * pd.m - (ib + Kk - Ll) * pd.n;
+      return dev > lim || dev < -lim;
+    };
     const int Kb = K - 16;
     // key window: lane l's bit i = its cell at row Kb + i - l: bit q of the
     // column {0, vd[3], vd[2], vd[1], vd[0], 0} (rows below / above the tile read 0)
@@ -357,6 +381,10 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
       if (L > bnd) break;  // the cell is below the tile's rows or past its columns
       const int i = K - Kb;
       if ((unsigned)i > 31u) break;  // off the key window: a new tile here
+      if (wchk && outside(L, K)) {
+        out = true;
+        break;
+      }
       if (K != Kc) {
         Dm = __builtin_amdgcn_ballot_w64((WD >> i) & 1u);
         Um = __builtin_amdgcn_ballot_w64(!((WU >> i) & 1u));
@@ -365,6 +393,10 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
       const int lend = bnd + 1;  // first lane past the readable cells of this key
       const u64 stops = ~Dm & (~0ull << L);
       const int ls = sminu(sff1u(stops), lend);  // (no stop: ff1 = -1)
+      if (wchk && outside(ls < lend ? ls : lend - 1, K)) {  // the run's last cell read
+        out = true;
+        break;
+      }
       if (ls >= lend) {  // D moves through lanes L .. lend - 1
         L = lend;
         break;
@@ -377,6 +409,10 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
         const int jlo = smax(trowlo + ls - Kb, 0);  // lowest key bit inside the tile's rows
         const unsigned below = i >= 31 ? ~0u : ((2u << i) - 1u);
         const unsigned stopm = (wd | wu) & below & ~((1u << jlo) - 1u);
+        if (wchk && outside(ls, Kb + (stopm ? 31 - __builtin_clz(stopm) : jlo))) {  // the vertical run's last cell
+          out = true;
+          break;
+        }
         if (stopm == 0u) {  // the run leaves the tile's rows (or the key window): U moves down to there
           const int nU = i - jlo + 1;
           nUv = writelane(nUv, nU, ls);
@@ -451,13 +487,21 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
   (void)prog;
 }
 
+// Waves per SIMD the kernel is compiled for (NWK_COL_WPE; register budget 512 / WPE)
+#ifndef NWK_COL_WPE
+#define NWK_COL_WPE 4
+#endif
+#define NWK_COL_OCC __attribute__((amdgpu_waves_per_eu(NWK_COL_WPE)))
+
 // FUSE: the instantiation with the fused finalize (FillArgs::fuse_fin)
 template <int NP, int SR, bool FUSE>
-__global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_col(FillArgs a) {
+__global__ __launch_bounds__(256) NWK_COL_OCC void nw_align_col(FillArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char obuf_all[4][kTraceRing];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   unsigned* prog = a.prog ? a.prog + blockIdx.x * 4 + wid : nullptr;  // NWK_WATCHDOG markers
+  // verbose >= 2 timeline (FillArgs::stamps, layout in nwk_runtime.cpp)
+  if (a.stamps && threadIdx.x == 0) atomicMin(a.stamps + 11 * a.ntasks_pairs, (u64)__builtin_amdgcn_s_memrealtime());
 
   for (;;) {
     if constexpr (FUSE) {  // queued pairs to hash: whole groups between fill tasks
@@ -474,10 +518,14 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_col(FillArgs a) {
       return;
     }
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)a.err, BITS_RLX)) != 0u) return;
+    const u64 t_task = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
     const int2 task = a.tasks[tk];
     const PairDesc pd = a.pairs[task.x];
     const int band = task.y;
     const int R0 = band * kBR;
+    // the longest spans of a span-bound batch issue ahead of the other fill waves
+    if (pd.prio) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(0);
     // code bit planes of rows R0 + 32 lane + b (rows past m: code 0, never traced)
     unsigned x0 = 0, x1 = 0;
     {
@@ -506,6 +554,12 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_col(FillArgs a) {
     u64* gout = a.bnd + pd.bnd_off + (int64_t)band * nw * NP;
     const int nblk = pd.bits_nblk, blo = bits_blk_lo(band, pd.m, pd.n, pd.bits_w);
     unsigned* mb = a.mat + pd.mat_off + (int64_t)band * nblk * 1024 + lane * 4;
+    // windowed storage, per lane and 8-step block: its words hold rows R0 + 32 lane ..
+    // + 31 at columns s0 - lane .. + 7, so dev = c m - i n spans [hi - 7 m - 31 n, hi]
+    // with hi = (s0 - lane + 7) m - (R0 + 32 lane) n = s0 m + hi0 (bits_lane_stored)
+    const bool win = pd.bits_w > 0;
+    const int64_t lim = (int64_t)pd.bits_w * pd.m, hlim = lim + 7ll * pd.m + 31ll * pd.n;
+    const int64_t hi0 = (int64_t)(7 - lane) * pd.m - (int64_t)(R0 + 32 * lane) * pd.n;
     // y windows: lane t's window for the half starting at step s_h is position s_h - t
     const unsigned* ywp = a.yw + 2 * (pd.e_off - (int64_t)lane);
     unsigned wc0 = ywp[0], wc1 = ywp[1];
@@ -517,6 +571,7 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_col(FillArgs a) {
     u64 g = 0;
     if (from_above) g = __hip_atomic_load((gu64*)(gin + gk), BITS_RLX);
     bool ok = true;
+    u64 cyc_wait = 0, cyc_wait0 = 0, n_wait = 0;  // (verbose >= 2 timeline)
 
     auto half = [&](int h, auto mask_t) {
       constexpr bool MASK = decltype(mask_t)::value;
@@ -525,7 +580,14 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_col(FillArgs a) {
       if (from_above) {
         if (h < nw) {
           if (!wall(!gl || (unsigned)(g >> 32) == a.epoch)) {
+            const u64 tw = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
             g = bits_wait(gin + (int64_t)h * NP + gk, gl, a.epoch, g, a.err);
+            if (a.stamps) {
+              const u64 d = __builtin_amdgcn_s_memtime() - tw;
+              cyc_wait += d;
+              if (h == 0) cyc_wait0 = d;
+              ++n_wait;
+            }
             // (a failed wait ends the task after this half, which publishes nothing; the
             // error word fails the call.  No early return: it would leave the carries
             // undefined on one path, and the compiler then moves them out of SGPRs)
@@ -544,7 +606,9 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_col(FillArgs a) {
         constexpr int B = decltype(bc)::value;
         const int s0 = 32 * h + 8 * B;
         const int rel = (s0 >> 3) - blo;
-        const bool sto = (unsigned)rel < (unsigned)nblk;
+        // stored: the block is among the band's stored steps and (windowed) this
+        // lane's words of it hold a cell within bits_w columns of the diagonal
+        const bool sto = (unsigned)rel < (unsigned)nblk && (!win || bits_lane_stored(hi0 + (int64_t)s0 * pd.m, lim, hlim));
         unsigned* st = mb + (int64_t)rel * 1024;
         col_block<NP, SR, MASK, B == 3, B>(s0, lane, x0, x1, wc0, wc1, l, c, acc, inj, pub, st, sto);
       };
@@ -573,6 +637,13 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_col(FillArgs a) {
     }
     BITS_PROG(0x30000000u);
     if (!ok) return;
+    if (a.stamps && lane == 0) {  // per pair: band cycles
+      atomicAdd(a.stamps + 8 * pd.slot + 6, (u64)(__builtin_amdgcn_s_memtime() - t_task));
+      atomicAdd(a.stamps + 8 * pd.slot + 7, cyc_wait);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot, cyc_wait0);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 1, n_wait);
+      atomicAdd(a.stamps + 8 * a.ntasks_pairs + 3 * pd.slot + 2, (u64)nsb);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -587,7 +658,14 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_col(FillArgs a) {
       int tlen;
       int2 tend;
       bool tout;
+      // the walk is one wave's chain of dependent scalar instructions, and the fill
+      // waves around it issue ~24 scalar instructions a step: it goes first
+      // (NWK_COL_TRACE_PRIO=0 at build time: no raise, for A/B)
+#if !defined(NWK_COL_TRACE_PRIO) || NWK_COL_TRACE_PRIO
+      __builtin_amdgcn_s_setprio(3);
+#endif
       trace_col(a, pd, obuf_all[wid], lane, prog, tlen, tend, tout);
+      __builtin_amdgcn_s_setprio(0);
       if constexpr (FUSE) {
         const bool ok_rows = !tout && fin_rows(a, pd, lane, tlen, tend);
         hq_push(a, pd, lane, ok_rows);

@@ -66,7 +66,8 @@ struct PairDesc {
   // wave sweeps all bands of the pair as a rolling 2048-row strip -- lane bit p
   // runs rows p, p + 2048, ... with virtual column v = s - p, pass v / n',
   // column v % n' (0 = banded tasks)
-  int32_t bits_np, pad_;
+  int32_t bits_np;
+  int32_t prio;     // kCol: issue priority (s_setprio) of the pair's fill tasks -- the longest spans of a span-bound batch
   int64_t xw_off;   // kBitsStrip: y-window index of the row sequence's position 0 (its row codes)
 };
 

@@ -1165,6 +1165,25 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     static const int strip_win_env = getenv("NWK_STRIP_WIN") ? atoi(getenv("NWK_STRIP_WIN")) : 1024;
     if (W == 0 && pl.mode == kBitsStrip) W = strip_win_env;
     set_w(W);
+    // nw_align_col stores 512 B per wave-step; at full storage a batch of many
+    // concurrent bands writes faster than HBM takes it (C3's 8-rank shard and
+    // big13 fit in full and wrote ~4-6 TB/s), so it keeps a window even when
+    // full storage fits: per pair W = 2.5 x the paths' expected stray from the
+    // diagonal, ~400 (n / 8000)^(2/3) columns for random sequences (max |dev|
+    // over sampled pairs: 361 at C4's 8k, 1165 at C3's 50k,
+    // profiles/r02/pathdev_*.txt), at least 1024 and at most a budget-forced W.
+    // A path that strays further re-runs with full storage.  NWK_COL_WIN:
+    // 0 = full storage when it fits, W > 0 forced.
+    static const int col_win_env = getenv("NWK_COL_WIN") ? atoi(getenv("NWK_COL_WIN")) : -1;
+    if (pl.mode == kCol && win_env < 0 && col_win_env != 0) {
+      for (auto& w : dp) {
+        const double est = 400.0 * std::pow(std::max(w.m, w.n) / 8000.0, 2.0 / 3.0);
+        int wc = col_win_env > 0 ? col_win_env : (int)round_up(std::max<int64_t>(1024, (int64_t)(2.5 * est)), 256);
+        if (W > 0) wc = std::min(wc, W);
+        w.bits_w = wc;
+        footprint(&w, pl.bits, pl.mode, sc.affine);
+      }
+    }
   }
   st.window = dp.empty() ? 0 : dp[0].bits_w;
   // Largest first (LPT inside the device; longest bands dequeued first).
@@ -1338,7 +1357,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       d.e_off = bitsy ? c->yw_off[w.j] : c->e_off[w.j];
       d.xw_off = pl.mode == kBitsStrip ? c->yw_off[w.i] : 0;
       d.bits_np = pl.mode == kBitsStrip ? strip_np(w.n) : 0;
-      d.pad_ = 0;
+      d.prio = 0;
       d.mat_off = mat_base_b / 4 + mo;
       d.bnd_off = bo;
       d.ops_off = ops_base_b + oo;
@@ -1366,6 +1385,16 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       mo += w.mat_dw; bo += w.bnd_gr; oo += w.ops_b;
       ntasks += tasks_of(pl.mode, d.nbands);
       maxb = std::max(maxb, (int)tasks_of(pl.mode, d.nbands));
+    }
+    // kCol, span-bound batches (under two rounds of tasks per wave slot, e.g.
+    // big13): a pair costs at least its span n + ~100 x bands steps, so the
+    // pairs with the longest spans get issue priority over the rest (their
+    // waves then step at nearly a lone wave's rate).  NWK_COL_PRIO=0 disables.
+    static const int col_prio_env = getenv("NWK_COL_PRIO") ? atoi(getenv("NWK_COL_PRIO")) : 1;
+    if (pl.mode == kCol && col_prio_env != 0 && ntasks <= 2 * (int64_t)grid * 4) {
+      double smax = 0;
+      for (int q = 0; q < np; ++q) smax = std::max(smax, (double)pd[q].n + 100.0 * pd[q].nbands);
+      for (int q = 0; q < np; ++q) pd[q].prio = (double)pd[q].n + 100.0 * pd[q].nbands >= 0.7 * smax ? 2 : 0;
     }
     if ((rc = c->h_tasks.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
     int2* tk = c->h_tasks.as<int2>();

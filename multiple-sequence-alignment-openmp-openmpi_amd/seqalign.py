@@ -19,7 +19,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libnwk.so")
+# NWK_LIB: an A/B build variant of the library (tools/col_variant.sh); default the in-tree build
+LIB_PATH = os.environ.get("NWK_LIB") or os.path.join(HERE, "lib", "libnwk.so")
 
 NWK_OK = 0
 ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "EKERNEL", -5: "ECOMM"}
