@@ -360,17 +360,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import seqalign
 
-    dist = None
-    coll_device = None
+    comm = None
     gpu = local
-    # NWK_BENCH_FORCE_DIST=1 (tests): the sharded path -- process group, LPT
-    # shard, the one all-gather -- even at WORLD_SIZE 1, so a 1-GPU box runs
-    # the RCCL collective the driver's N-GPU runs use
+    # NWK_BENCH_FORCE_DIST=1 (tests): the sharded path -- communicator, LPT
+    # shard, the all-gathers -- even at WORLD_SIZE 1, so a 1-GPU box runs the
+    # RCCL collective the driver's N-GPU runs use
     sharded = world > 1 or os.environ.get("NWK_BENCH_FORCE_DIST") == "1"
     if sharded:
-        import torch
-        import torch.distributed as tdist
-
         import dist as nwdist
 
         # Test hooks (not used by the driver): NWK_BENCH_BACKEND=gloo and
@@ -383,13 +379,15 @@ def main():
             sys.exit("bench.py: rank %d has no GPU (%d visible)" % (local, ndev))
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
-            torch.cuda.set_device(gpu)
-            tdist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-            coll_device = torch.device("cuda", gpu)
+            # RCCL through the library (nwk_comm_*): this process maps one HIP
+            # runtime and one RCCL, the library's -- torch is never imported here
+            comm = nwdist.rccl_comm(gpu, world, rank)
         else:
+            import torch.distributed as tdist
+
             tdist.init_process_group(backend)
-        dist = tdist
-        world = dist.get_world_size()  # n_gpus comes from the communicator
+            comm = nwdist.TorchComm()
+        world = comm.world  # n_gpus comes from the communicator
 
     name, pxy, pgap, genes, affine, expect = load_workload(args.workload)
     if args.affine is not None:
@@ -433,18 +431,18 @@ def main():
         t_step = time.perf_counter()
         if stream:
             h, pen, hs = nwdist.align_sharded_streamed(
-                eng, lengths, pxy, pgap, rank, world, chunks=chunks, device=coll_device,
+                eng, lengths, pxy, pgap, rank, world, chunks=chunks, comm=comm,
                 on_piece=lambda c: piece_t.append(round((time.perf_counter() - t_step) * 1e3, 3)))
             piece_stats.append(eng.stats())  # (the call has ended inside)
         elif sharded and not affine:
             h, pen, hs = nwdist.align_sharded_pipelined(eng, lengths, pxy, pgap, rank, world, chunks=chunks,
-                                                       device=coll_device,
+                                                       comm=comm,
                                                        on_piece=lambda c: (piece_stats.append(eng.stats()),
                                                                            piece_t.append(round(
                                                                                (time.perf_counter() - t_step) * 1e3,
                                                                                3))))
         elif sharded:
-            pen, hs, _ = nwdist.align_sharded(align, lengths, pxy, pgap, rank, world, device=coll_device)
+            pen, hs, _ = nwdist.align_sharded(align, lengths, pxy, pgap, rank, world, comm=comm)
             h = seqalign.chain_hash(hs) if rank == 0 else None
             piece_stats.append(eng.stats())
         else:  # getMinimumPenalties on the engine: the chain overlaps later batches
@@ -455,11 +453,8 @@ def main():
 
     def sync():
         if sharded:
-            import torch
-
-            dist.barrier()
-            if torch.cuda.is_available():
-                torch.cuda.synchronize()
+            comm.barrier()
+            seqalign.device_synchronize(gpu)
 
     def check(pen, h):
         if rank != 0 or expect is None:
@@ -482,14 +477,10 @@ def main():
     dt = time.perf_counter() - t0
     checks.append(check(pen, h))  # the last timed step's answer
     if sharded:
-        import torch
-
-        t = torch.tensor([dt], dtype=torch.float64, device=coll_device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = comm.max(dt)  # the slowest rank's time
     if rank != 0:
-        dist.destroy_process_group()
         eng.close()
+        comm.close()
         return
 
     ms_step = dt / max(args.steps, 1) * 1e3
@@ -538,7 +529,7 @@ def main():
                              fill_ms / launches * 1e-3, my_cells, launches),
     }
     if sharded:
-        out["collective"] = {"backend": dist.get_backend(), "all_gathers_per_step": 1 if affine else chunks,
+        out["collective"] = {"backend": comm.backend, "all_gathers_per_step": 1 if affine else chunks,
                              "record_bytes": 72, "forced_at_world_1": world == 1,
                              "pieces_per_rank": 1 if affine else chunks,
                              "piece_ready_ms": list(piece_t)}  # rank 0, last timed step
@@ -550,9 +541,9 @@ def main():
         out["cpu_baseline"] = cpu_baseline(genes, pxy, pgap, affine, expect_pen=pen if ok_gpu else None,
                                            expect_hs=last_hs[0] if ok_gpu else None)
     print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
     eng.close()
+    if comm is not None:
+        comm.close()
     if answer_ok is False:
         sys.exit("bench.py: answer hash / penalties differ from " + expect["source"])
 

@@ -258,6 +258,29 @@ void nwk_chain_destroy(nwk_chain *ch);
 /* sw::sha512::calculate equivalent: lowercase hex digest of data[0..len). */
 void nwk_sha512_hex(const uint8_t *data, int64_t len, char *out_hex);
 
+/* ---- Multi-process collectives over RCCL (one process per GPU) ----------
+ * Replaces the reference's MPI exchange for the sharded path (sub:249-266
+ * broadcasts, sub:296-331 task / result messages): each rank process aligns
+ * its shard on its own device and the fixed-size result records travel by
+ * ncclAllGather over xGMI.  The communicator lives in this library, so a rank
+ * process binds exactly one HIP runtime and one RCCL (no second copy brought
+ * in by a Python framework).  Rank 0 makes the id (NWK_COMM_ID_BYTES opaque
+ * bytes) and hands it to the other ranks out of band; nwk_comm_create is
+ * collective over all ranks.  Buffers are host memory; the library stages them
+ * through device memory on its own stream, and every call returns after the
+ * collective has completed. */
+#define NWK_COMM_ID_BYTES 128
+typedef struct nwk_comm nwk_comm;
+int nwk_comm_unique_id(uint8_t *id);
+int nwk_comm_create(int32_t device, const uint8_t *id, int32_t world, int32_t rank, nwk_comm **out);
+/* recv (world x bytes) = every rank's send block (bytes), in rank order */
+int nwk_comm_all_gather(nwk_comm *comm, const void *send, int64_t bytes, void *recv);
+/* vals[0..n) = the maximum over ranks, element-wise (also a barrier) */
+int nwk_comm_all_reduce_max_f64(nwk_comm *comm, double *vals, int64_t n);
+void nwk_comm_destroy(nwk_comm *comm);
+/* hipDeviceSynchronize on the device (the bench's timed-region brackets) */
+int nwk_device_synchronize(int32_t device);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2373,6 +2373,114 @@ static int min_penalties_sc(const uint8_t* seqs, const int64_t* offsets, int32_t
 }
 
 // ---------------------------------------------------------------------------
+// Multi-process communicator (nwk_comm_*): one RCCL rank per process.
+// ---------------------------------------------------------------------------
+struct nwk_comm {
+  int device = 0, world = 0, rank = 0;
+  ncclComm_t comm = nullptr;
+  hipStream_t stream = nullptr;
+  void* dbuf = nullptr;  // staging: send block | world x recv blocks
+  size_t dcap = 0;
+};
+
+static_assert(sizeof(ncclUniqueId) <= NWK_COMM_ID_BYTES, "ncclUniqueId larger than NWK_COMM_ID_BYTES");
+
+int nwk_comm_unique_id(uint8_t* id) {
+  if (!id) return fail(NWK_EINVAL, "nwk_comm_unique_id: id is NULL");
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return fail(NWK_ECOMM, "ncclGetUniqueId failed");
+  memset(id, 0, NWK_COMM_ID_BYTES);
+  memcpy(id, &u, sizeof(u));
+  return NWK_OK;
+}
+
+int nwk_comm_create(int32_t device, const uint8_t* id, int32_t world, int32_t rank, nwk_comm** out) {
+  if (!id || !out || world < 1 || rank < 0 || rank >= world) return fail(NWK_EINVAL, "nwk_comm_create: bad argument");
+  *out = nullptr;
+  if (device < 0 || device >= nwk_device_count()) return fail(NWK_EDEVICE, "nwk_comm_create: no device %d", device);
+  auto* cm = new nwk_comm;
+  cm->device = device;
+  cm->world = world;
+  cm->rank = rank;
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&cm->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete cm;
+    return fail(NWK_EDEVICE, "nwk_comm_create: device %d", device);
+  }
+  if (ncclCommInitRank(&cm->comm, world, u, rank) != ncclSuccess) {
+    (void)hipStreamDestroy(cm->stream);
+    delete cm;
+    return fail(NWK_ECOMM, "ncclCommInitRank failed (rank %d of %d)", rank, world);
+  }
+  *out = cm;
+  return NWK_OK;
+}
+
+static int comm_stage(nwk_comm* cm, size_t bytes) {
+  if (bytes <= cm->dcap) return NWK_OK;
+  if (cm->dbuf) (void)hipFree(cm->dbuf);
+  cm->dbuf = nullptr;
+  cm->dcap = 0;
+  if (hipMalloc(&cm->dbuf, bytes) != hipSuccess) return fail(NWK_ENOMEM, "nwk_comm: staging buffer of %zu bytes", bytes);
+  cm->dcap = bytes;
+  return NWK_OK;
+}
+
+int nwk_comm_all_gather(nwk_comm* cm, const void* send, int64_t bytes, void* recv) {
+  if (!cm || bytes < 0 || (bytes > 0 && (!send || !recv))) return fail(NWK_EINVAL, "nwk_comm_all_gather: bad argument");
+  if (hipSetDevice(cm->device) != hipSuccess) return fail(NWK_EDEVICE, "nwk_comm_all_gather: device");
+  const size_t b = (size_t)std::max<int64_t>(bytes, 1);
+  int rc = comm_stage(cm, b * (size_t)(cm->world + 1));
+  if (rc != NWK_OK) return rc;
+  uint8_t* ds = static_cast<uint8_t*>(cm->dbuf);
+  uint8_t* dr = ds + b;
+  if (bytes > 0) HIP_TRY(hipMemcpyAsync(ds, send, (size_t)bytes, hipMemcpyHostToDevice, cm->stream));
+  if (ncclAllGather(ds, dr, b, ncclUint8, cm->comm, cm->stream) != ncclSuccess)
+    return fail(NWK_ECOMM, "ncclAllGather failed (rank %d)", cm->rank);
+  if (bytes > 0) {
+    if (b == (size_t)bytes) {
+      HIP_TRY(hipMemcpyAsync(recv, dr, b * cm->world, hipMemcpyDeviceToHost, cm->stream));
+    } else {
+      for (int r = 0; r < cm->world; ++r)
+        HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(recv) + (size_t)bytes * r, dr + b * r, (size_t)bytes,
+                               hipMemcpyDeviceToHost, cm->stream));
+    }
+  }
+  HIP_TRY(hipStreamSynchronize(cm->stream));
+  return NWK_OK;
+}
+
+int nwk_comm_all_reduce_max_f64(nwk_comm* cm, double* vals, int64_t n) {
+  if (!cm || n < 1 || !vals) return fail(NWK_EINVAL, "nwk_comm_all_reduce_max_f64: bad argument");
+  if (hipSetDevice(cm->device) != hipSuccess) return fail(NWK_EDEVICE, "nwk_comm_all_reduce_max_f64: device");
+  int rc = comm_stage(cm, sizeof(double) * (size_t)n);
+  if (rc != NWK_OK) return rc;
+  HIP_TRY(hipMemcpyAsync(cm->dbuf, vals, sizeof(double) * n, hipMemcpyHostToDevice, cm->stream));
+  if (ncclAllReduce(cm->dbuf, cm->dbuf, (size_t)n, ncclFloat64, ncclMax, cm->comm, cm->stream) != ncclSuccess)
+    return fail(NWK_ECOMM, "ncclAllReduce failed (rank %d)", cm->rank);
+  HIP_TRY(hipMemcpyAsync(vals, cm->dbuf, sizeof(double) * n, hipMemcpyDeviceToHost, cm->stream));
+  HIP_TRY(hipStreamSynchronize(cm->stream));
+  return NWK_OK;
+}
+
+void nwk_comm_destroy(nwk_comm* cm) {
+  if (!cm) return;
+  (void)hipSetDevice(cm->device);
+  if (cm->comm) ncclCommDestroy(cm->comm);
+  if (cm->dbuf) (void)hipFree(cm->dbuf);
+  if (cm->stream) (void)hipStreamDestroy(cm->stream);
+  delete cm;
+}
+
+int nwk_device_synchronize(int32_t device) {
+  if (device < 0 || device >= nwk_device_count()) return fail(NWK_EDEVICE, "nwk_device_synchronize: no device %d", device);
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipDeviceSynchronize());
+  return NWK_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Progressive sum-of-pairs MSA (build-defined, oracle
 // oracle/msa_oracle.c nwo_msa): UPGMA on the pairwise penalties, then one
 // profile-profile DP per merge on the GPU (nw_profile + the fused affine-code

@@ -14,10 +14,15 @@ Failure contract (the C++ in-process path tags records the same way): a rank
 whose alignment raises still contributes its block, every record tagged
 FAILED, to the one collective; every rank then raises RankFailed instead of
 some ranks hanging in the all-gather.
+
+Communicators: RcclComm (the GPU ranks: RCCL through the library's own
+nwk_comm_*, so a rank process maps one HIP runtime and one RCCL and never
+imports torch) or TorchComm (torch.distributed: gloo in the CPU tests).
 """
+import os
+import time
+
 import numpy as np
-import torch
-import torch.distributed as dist
 
 import seqalign
 
@@ -74,15 +79,108 @@ def unpack_records(gathered, P):
     return pen, hs
 
 
-def all_gather_records(rec, device=None, group=None):
+class TorchComm:
+    """torch.distributed as the communicator (gloo on CPU in the tests)."""
+
+    def __init__(self, group=None, device=None):
+        import torch.distributed as tdist
+
+        self.dist, self.group, self.device = tdist, group, device
+        self.world = tdist.get_world_size(group)
+        self.rank = tdist.get_rank(group)
+        self.backend = tdist.get_backend(group)
+
+    def all_gather(self, rec):
+        import torch
+
+        t = torch.from_numpy(np.ascontiguousarray(rec))
+        if self.device is not None:
+            t = t.to(self.device, non_blocking=False)
+        out = torch.empty((self.world * rec.shape[0],) + tuple(rec.shape[1:]), dtype=t.dtype, device=t.device)
+        self.dist.all_gather_into_tensor(out, t, group=self.group)
+        return out.cpu().numpy()
+
+    def max(self, x):
+        import torch
+
+        t = torch.tensor([float(x)], dtype=torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())
+
+    def barrier(self):
+        self.dist.barrier(group=self.group)
+
+    def close(self):
+        pass
+
+
+class RcclComm:
+    """RCCL through libnwk (seqalign.Comm): the GPU ranks' communicator."""
+
+    backend = "rccl (nwk_comm)"
+
+    def __init__(self, comm):
+        self.comm = comm
+        self.world, self.rank = comm.world, comm.rank
+
+    def all_gather(self, rec):
+        g = self.comm.all_gather(rec)
+        return g.reshape((self.world * rec.shape[0],) + tuple(rec.shape[1:]))
+
+    def max(self, x):
+        return float(self.comm.all_reduce_max([float(x)])[0])
+
+    def barrier(self):
+        self.comm.barrier()
+
+    def close(self):
+        self.comm.close()
+
+
+def rccl_comm(device, world, rank, timeout_s=120.0):
+    """RcclComm for this rank process.  Rendezvous on the node: rank 0 writes
+    the RCCL id to a file named by the launcher (the ranks' common parent
+    process) and MASTER_PORT; the other ranks wait for it.  All ranks of a
+    bench run are on one node (torch.distributed.run --nnodes=1, or bench.py's
+    own spawn)."""
+    key = "%s_%s" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "nwk_rccl_id_%s" % key)
+    if rank == 0:
+        uid = seqalign.Comm.unique_id()
+        tmp = path + ".tmp%d" % os.getpid()
+        with open(tmp, "wb") as f:
+            f.write(uid)
+        os.replace(tmp, path)
+    else:
+        t0 = time.time()
+        while True:
+            try:
+                with open(path, "rb") as f:
+                    uid = f.read()
+                if len(uid) == seqalign.COMM_ID_BYTES:
+                    break
+            except OSError:
+                pass
+            if time.time() - t0 > timeout_s:
+                raise RuntimeError("rank %d: no RCCL id from rank 0 at %s after %.0f s" % (rank, path, timeout_s))
+            time.sleep(0.01)
+    comm = RcclComm(seqalign.Comm(device, uid, world, rank))
+    comm.barrier()  # every rank has read the id
+    if rank == 0:
+        try:
+            os.remove(path)
+        except OSError:
+            pass
+    return comm
+
+
+def default_comm(comm, device=None, group=None):
+    return comm if comm is not None else TorchComm(group, device)
+
+
+def all_gather_records(rec, device=None, group=None, comm=None):
     """ONE collective: every rank contributes `per` records."""
-    world = dist.get_world_size(group)
-    t = torch.from_numpy(rec)
-    if device is not None:
-        t = t.to(device, non_blocking=False)
-    out = torch.empty((world * rec.shape[0], REC), dtype=torch.uint8, device=t.device)
-    dist.all_gather_into_tensor(out, t, group=group)
-    return out.cpu().numpy()
+    return default_comm(comm, device, group).all_gather(rec)
 
 
 def unpack_chunk(gathered):
@@ -235,17 +333,13 @@ class StreamedShard:
         return self.err
 
 
-def any_rank_failed(failed, device=None, group=None):
-    """One status collective (all_reduce MAX of a flag): True on every rank
+def any_rank_failed(failed, comm):
+    """One status collective (all-reduce MAX of a flag): True on every rank
     when any rank failed."""
-    import torch
-
-    t = torch.tensor([1 if failed else 0], dtype=torch.int32, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-    return bool(int(t.item()))
+    return comm.max(1.0 if failed else 0.0) > 0.0
 
 
-def _exchange(shard, chunks, rank, P, device, group, final_status):
+def _exchange(shard, chunks, rank, P, comm, final_status):
     """The collective side shared by both pipelines: one all-gather per piece,
     rank 0's chain worker fed per piece as it arrives (sub:305-331 collects
     results as they arrive, sub:334-337 chains)."""
@@ -254,7 +348,7 @@ def _exchange(shard, chunks, rank, P, device, group, final_status):
     try:
         shard.start()
         for c in range(chunks):
-            g = all_gather_records(shard.block(c), device=device, group=group)
+            g = comm.all_gather(shard.block(c))
             if err is not None or shard.err is not None:
                 continue
             try:
@@ -266,7 +360,7 @@ def _exchange(shard, chunks, rank, P, device, group, final_status):
                 chain.feed(cid, cpen, chs)
         own = shard.finish()
         err = own if own is not None else err
-        if final_status and any_rank_failed(err is not None, device=device, group=group) and err is None:
+        if final_status and any_rank_failed(err is not None, comm) and err is None:
             err = RankFailed("a peer rank failed after the last piece was exchanged")
         if err is not None:
             raise RankFailed("rank %d: %s" % (rank, err)) from err
@@ -280,7 +374,7 @@ def _exchange(shard, chunks, rank, P, device, group, final_status):
 
 
 def align_sharded_pipelined(eng, lengths, pxy, pgap, rank, world, chunks=1, device=None, group=None,
-                            on_piece=None):
+                            on_piece=None, comm=None):
     """The shard in `chunks` pieces of ascending canonical ids: piece c+1 aligns
     on the GPU (Engine.align_pairs_begin) while piece c's records go through
     their all-gather and rank 0's chain worker (seqalign.ChainStream) advances
@@ -294,11 +388,11 @@ def align_sharded_pipelined(eng, lengths, pxy, pgap, rank, world, chunks=1, devi
     P = k * (k - 1) // 2
     parts, per = chunk_parts(lengths, rank, world, chunks)
     shard = PipelinedShard(eng, parts, per, pxy, pgap, on_piece=on_piece)
-    return _exchange(shard, chunks, rank, P, device, group, final_status=False)
+    return _exchange(shard, chunks, rank, P, default_comm(comm, device, group), final_status=False)
 
 
 def align_sharded_streamed(eng, lengths, pxy, pgap, rank, world, chunks=8, device=None, group=None,
-                           on_piece=None, poll_s=50e-6):
+                           on_piece=None, poll_s=50e-6, comm=None):
     """The shard as ONE launch whose per-pair records stream to the host as
     pairs are hashed inside the fill launch (StreamedShard).  Piece c -- the
     shard's ids below the global threshold P (c+1) / chunks -- goes through its
@@ -312,7 +406,7 @@ def align_sharded_streamed(eng, lengths, pxy, pgap, rank, world, chunks=8, devic
     P = k * (k - 1) // 2
     parts, per = chunk_parts(lengths, rank, world, chunks)
     shard = StreamedShard(eng, parts, per, pxy, pgap, poll_s=poll_s, on_piece=on_piece)
-    return _exchange(shard, chunks, rank, P, device, group, final_status=True)
+    return _exchange(shard, chunks, rank, P, default_comm(comm, device, group), final_status=True)
 
 
 def emulate_ranks(make_shard, world, chunks, P):
@@ -346,7 +440,7 @@ def emulate_ranks(make_shard, world, chunks, P):
     return h, pen, hs, ready
 
 
-def align_sharded(align_fn, lengths, pxy, pgap, rank, world, device=None, group=None):
+def align_sharded(align_fn, lengths, pxy, pgap, rank, world, device=None, group=None, comm=None):
     """Runs this rank's shard through align_fn(ids, pxy, pgap) -> (pen, hashes),
     gathers every rank's records and returns (penalties[P], hashes[P,64], ids)."""
     k = len(lengths)
@@ -360,7 +454,7 @@ def align_sharded(align_fn, lengths, pxy, pgap, rank, world, device=None, group=
     except Exception as e:  # still join the ONE collective, so no peer waits forever
         err = e
         rec = failed_block(per)
-    g = all_gather_records(rec, device=device, group=group)
+    g = all_gather_records(rec, device=device, group=group, comm=comm)
     if err is not None:
         raise RankFailed("rank %d: %s" % (rank, err)) from err
     pen_all, hs_all = unpack_records(g, P)

@@ -86,7 +86,14 @@ SIGNATURES = {
     "nwk_chain_feed": (ctypes.c_int, [_P, _P, _P, _P, _I64]),
     "nwk_chain_finish": (ctypes.c_int, [_P, _P, _P, _P]),
     "nwk_chain_destroy": (None, [_P]),
+    "nwk_comm_unique_id": (ctypes.c_int, [_P]),
+    "nwk_comm_create": (ctypes.c_int, [_I32, _P, _I32, _I32, _P]),
+    "nwk_comm_all_gather": (ctypes.c_int, [_P, _P, _I64, _P]),
+    "nwk_comm_all_reduce_max_f64": (ctypes.c_int, [_P, _P, _I64]),
+    "nwk_comm_destroy": (None, [_P]),
+    "nwk_device_synchronize": (ctypes.c_int, [_I32]),
 }
+COMM_ID_BYTES = 128
 
 _lib = None
 
@@ -372,6 +379,58 @@ class ChainStream:
             self.close()
         except Exception:
             pass
+
+
+class Comm:
+    """nwk_comm_*: one RCCL rank of a multi-process job, held by the library
+    (the rank process binds only the library's HIP runtime and RCCL).  The
+    rendezvous -- rank 0's id handed to the others -- is the caller's
+    (dist.rccl_comm does it through a file on the node)."""
+
+    def __init__(self, device, uid, world, rank):
+        self.lib = load_library()
+        self.device, self.world, self.rank = device, world, rank
+        self._c = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(bytes(uid).ljust(COMM_ID_BYTES, b"\0"))
+        _check(self.lib.nwk_comm_create(device, buf, world, rank, ctypes.byref(self._c)))
+
+    @staticmethod
+    def unique_id():
+        lib = load_library()
+        buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
+        _check(lib.nwk_comm_unique_id(buf))
+        return bytes(buf)
+
+    def all_gather(self, block):
+        """block: a C-contiguous numpy array (the same shape on every rank) ->
+        (world,) + block.shape, every rank's block in rank order."""
+        b = np.ascontiguousarray(block)
+        out = np.empty((self.world,) + b.shape, dtype=b.dtype)
+        _check(self.lib.nwk_comm_all_gather(self._c, _ptr(b), b.nbytes, _ptr(out)))
+        return out
+
+    def all_reduce_max(self, values):
+        v = np.ascontiguousarray(values, dtype=np.float64).copy()
+        _check(self.lib.nwk_comm_all_reduce_max_f64(self._c, _ptr(v), v.size))
+        return v
+
+    def barrier(self):
+        self.all_reduce_max(np.zeros(1))
+
+    def close(self):
+        if self._c:
+            self.lib.nwk_comm_destroy(self._c)
+            self._c = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def device_synchronize(device):
+    _check(load_library().nwk_device_synchronize(int(device)))
 
 
 def chain_hash(problem_hashes):

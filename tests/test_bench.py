@@ -81,12 +81,13 @@ def test_two_ranks_share_one_gpu_big13_published_hash():
 
 @pytest.mark.gpu
 def test_bench_nccl_all_gather_at_world_one():
-    """The driver's multi-GPU bench path with the real backend: torch.distributed
-    over "nccl" (= RCCL), LPT shard, ONE all_gather_into_tensor of the 72-byte
-    records and the max-over-ranks all_reduce, forced at WORLD_SIZE 1
+    """The driver's multi-GPU bench path with the real backend: RCCL through the
+    library's communicator (nwk_comm_*: ncclCommInitRank after a file
+    rendezvous on the node), LPT shard, the all-gather of the 72-byte records
+    and the max-over-ranks all-reduce, forced at WORLD_SIZE 1
     (NWK_BENCH_FORCE_DIST) so it runs on a 1-GPU box; big13's published hash.
-    The JSON line names the HIP runtime and RCCL the process mapped (torch is
-    imported first, so libnwk.so binds to torch's)."""
+    The rank process never imports torch: it maps exactly one HIP runtime,
+    one HSA runtime and one RCCL (the ones libnwk.so links)."""
     import socket
 
     s = socket.socket()
@@ -101,10 +102,11 @@ def test_bench_nccl_all_gather_at_world_one():
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.decode().strip().split("\n")[-1])
     assert line["answer_hash_ok"] is True
-    assert line["collective"]["backend"] == "nccl"
+    assert line["collective"]["backend"].startswith("rccl")
     libs = line["runtime_libs"]
     print("runtime libraries mapped:", libs)
-    assert any("librccl" in x for x in libs) and any("libamdhip64" in x for x in libs)
+    for name in ("librccl", "libamdhip64", "libhsa-runtime64"):
+        assert len([x for x in libs if name in os.path.basename(x)]) == 1, (name, libs)
     out = os.path.join(REPO, "gpurun_out")
     if os.path.isdir(out):
         with open(os.path.join(out, "bench_nccl_world1.json"), "w") as f:
