@@ -215,7 +215,126 @@ __device__ __forceinline__ int smax(int a, int b) {
   return r;
 }
 
-// Traceback of one pair from (m, n) over the stored (diag, up) bits.
+// The run loop of a pass without window checks, as one block of scalar code
+// (the compiled loop spends ~65 instructions and 8 branches on a stop, this
+// one ~25): the walk of trace_col's `walk` lambda, step for step.
+//   loop:  bnd = min(K - trowlo, LL); L > bnd or K - Kb > 31: done
+//          Dm, Um = the key's D and U lanes (v_bfe + v_cmp per mask)
+//          ls = min(ff1(~Dm & -1 << L), bnd + 1); ls > bnd: L = ls, done (a D run)
+//          U at ls: down lane ls's column (readlane of WD, WU): U^nU, then D
+//          (K = Kb + j, loop) or L (finL[ls], K = Kb + j + 1, lrun), or the run
+//          leaves the window (L = ls, K = Kb + jlo - 1, done)
+//          else L at ls: finL[ls], L = ls + 1, K + 1, lrun
+//   lrun:  rr = K - L; lend = min(LL, 31 + Kb - rr) + 1; L >= lend: loop
+//          le = min(ff1(~Lm & -1 << L), lend) over the row's L cells (WL at bit rr - Kb + lane)
+//          finL |= bits L .. le - 1; L = le; K = rr + le; loop
+__device__ __forceinline__ void walk_asm(unsigned WD, unsigned WU, unsigned WL, int lane, int Kb, int trowlo, int LL,
+                                         int& K, int& L, u64& finL, unsigned& nUv, int& maxU) {
+  int bnd, i, ls, t, j, nU;
+  unsigned wd, wu, sm;
+  u64 Dm, Um, m64;
+  unsigned vt;
+  asm volatile(
+      "s_nop 1\n"
+      "Lwloop%=:\n\t"
+      "s_sub_i32 %[bnd], %[K], %[trowlo]\n\t"
+      "s_min_i32 %[bnd], %[bnd], %[LL]\n\t"
+      "s_cmp_gt_i32 %[L], %[bnd]\n\t"
+      "s_cbranch_scc1 Lwdone%=\n\t"
+      "s_sub_i32 %[i], %[K], %[Kb]\n\t"
+      "s_cmp_gt_u32 %[i], 31\n\t"
+      "s_cbranch_scc1 Lwdone%=\n\t"
+      "v_bfe_u32 %[vt], %[WD], %[i], 1\n\t"
+      "v_cmp_ne_u32_e64 %[Dm], 0, %[vt]\n\t"
+      "v_bfe_u32 %[vt], %[WU], %[i], 1\n\t"
+      "v_cmp_eq_u32_e64 %[Um], 0, %[vt]\n\t"
+      "s_lshl_b64 %[m64], -1, %[L]\n\t"
+      "s_andn2_b64 %[m64], %[m64], %[Dm]\n\t"
+      "s_ff1_i32_b64 %[ls], %[m64]\n\t"
+      "s_add_i32 %[t], %[bnd], 1\n\t"
+      "s_min_u32 %[ls], %[ls], %[t]\n\t"
+      "s_cmp_gt_i32 %[ls], %[bnd]\n\t"
+      "s_cbranch_scc1 Lwdrun%=\n\t"
+      "s_bitcmp1_b64 %[Um], %[ls]\n\t"
+      "s_cbranch_scc1 Lwup%=\n\t"
+      // an L move at ls
+      "s_bitset1_b64 %[finL], %[ls]\n\t"
+      "s_add_i32 %[L], %[ls], 1\n\t"
+      "s_add_i32 %[K], %[K], 1\n\t"
+      "s_branch Lwlrun%=\n"
+      "Lwup%=:\n\t"
+      // a U move, then down lane ls's column while D is clear and U set
+      "v_readlane_b32 %[wd], %[WD], %[ls]\n\t"
+      "v_readlane_b32 %[wu], %[WU], %[ls]\n\t"
+      "s_add_i32 %[j], %[trowlo], %[ls]\n\t"
+      "s_sub_i32 %[j], %[j], %[Kb]\n\t"
+      "s_max_i32 %[j], %[j], 0\n\t"               // jlo
+      "s_lshl_b32 %[t], 2, %[i]\n\t"
+      "s_add_i32 %[t], %[t], -1\n\t"               // bits 0 .. i (2 << 31 wraps to 0: all)
+      "s_or_b32 %[sm], %[wd], %[wu]\n\t"
+      "s_and_b32 %[sm], %[sm], %[t]\n\t"
+      "s_lshl_b32 %[t], -1, %[j]\n\t"
+      "s_and_b32 %[sm], %[sm], %[t]\n\t"
+      "s_cmp_eq_u32 %[sm], 0\n\t"
+      "s_cbranch_scc1 Lwuleave%=\n\t"
+      "s_flbit_i32_b32 %[t], %[sm]\n\t"
+      "s_sub_i32 %[j], 31, %[t]\n\t"               // j: the key the vertical run stops at
+      "s_sub_i32 %[nU], %[i], %[j]\n\t"
+      "s_mov_b32 m0, %[ls]\n\t"
+      "v_writelane_b32 %[nUv], %[nU], m0\n\t"
+      "s_max_i32 %[maxU], %[maxU], %[nU]\n\t"
+      "s_add_i32 %[L], %[ls], 1\n\t"
+      "s_add_i32 %[K], %[Kb], %[j]\n\t"
+      "s_bitcmp1_b32 %[wd], %[j]\n\t"
+      "s_cbranch_scc1 Lwloop%=\n\t"                // ... then D
+      "s_bitset1_b64 %[finL], %[ls]\n\t"          // ... then L
+      "s_add_i32 %[K], %[K], 1\n"
+      "Lwlrun%=:\n\t"
+      // a horizontal run on row rr = K - L: the row's cells that move L, one ballot
+      "s_sub_i32 %[t], %[K], %[L]\n\t"             // rr
+      "s_sub_i32 %[j], %[Kb], %[t]\n\t"
+      "s_add_i32 %[j], %[j], 31\n\t"
+      "s_min_i32 %[j], %[j], %[LL]\n\t"
+      "s_add_i32 %[j], %[j], 1\n\t"                // lend
+      "s_cmp_ge_i32 %[L], %[j]\n\t"
+      "s_cbranch_scc1 Lwloop%=\n\t"
+      "s_sub_i32 %[nU], %[t], %[Kb]\n\t"
+      "v_add_u32_e32 %[vt], %[nU], %[lane]\n\t"
+      "v_bfe_u32 %[vt], %[WL], %[vt], 1\n\t"
+      "v_cmp_ne_u32_e64 %[Dm], 0, %[vt]\n\t"
+      "s_lshl_b64 %[m64], -1, %[L]\n\t"
+      "s_andn2_b64 %[m64], %[m64], %[Dm]\n\t"
+      "s_ff1_i32_b64 %[ls], %[m64]\n\t"
+      "s_min_u32 %[ls], %[ls], %[j]\n\t"           // le
+      "s_sub_i32 %[nU], %[ls], %[L]\n\t"
+      "s_bfm_b64 %[m64], %[nU], %[L]\n\t"          // lanes L .. le - 1
+      "s_or_b64 %[finL], %[finL], %[m64]\n\t"
+      "s_mov_b32 %[L], %[ls]\n\t"
+      "s_add_i32 %[K], %[t], %[ls]\n\t"
+      "s_branch Lwloop%=\n"
+      "Lwuleave%=:\n\t"
+      // the vertical run leaves the tile's rows (or the key window): U moves down to there
+      "s_sub_i32 %[nU], %[i], %[j]\n\t"
+      "s_add_i32 %[nU], %[nU], 1\n\t"
+      "s_mov_b32 m0, %[ls]\n\t"
+      "v_writelane_b32 %[nUv], %[nU], m0\n\t"
+      "s_max_i32 %[maxU], %[maxU], %[nU]\n\t"
+      "s_mov_b32 %[L], %[ls]\n\t"
+      "s_add_i32 %[K], %[Kb], %[j]\n\t"
+      "s_add_i32 %[K], %[K], -1\n\t"
+      "s_branch Lwdone%=\n"
+      "Lwdrun%=:\n\t"
+      "s_mov_b32 %[L], %[ls]\n"
+      "Lwdone%=:"
+      : [K] "+s"(K), [L] "+s"(L), [finL] "+s"(finL), [nUv] "+v"(nUv), [maxU] "+s"(maxU), [bnd] "=&s"(bnd),
+        [i] "=&s"(i), [ls] "=&s"(ls), [t] "=&s"(t), [j] "=&s"(j), [nU] "=&s"(nU), [wd] "=&s"(wd), [wu] "=&s"(wu),
+        [sm] "=&s"(sm), [Dm] "=&s"(Dm), [Um] "=&s"(Um), [m64] "=&s"(m64), [vt] "=&v"(vt)
+      : [WD] "v"(WD), [WU] "v"(WU), [WL] "v"(WL), [lane] "v"(lane), [Kb] "s"(Kb), [trowlo] "s"(trowlo), [LL] "s"(LL)
+      : "scc", "m0");
+}
+
+// Traceback of one pair from (m, n) over the stored (diag, up) bits
+// (SPEC = false), or a speculative segment of band sb (SPEC = true, below).
 //
 // Tiles are 64 columns (lane L holds column cts - L) by four row-lanes ta ..
 // ta - 3 (128 rows), eight dwords per lane: each lane loads its column's words
@@ -233,12 +352,37 @@ __device__ __forceinline__ int smax(int a, int b) {
 // its column is >= the band's lowest stored step (then its step, column +
 // row-lane, is stored too); a walk that leaves flags the pair for a re-run
 // with full storage.
-__device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd, unsigned char* obuf, int lane,
-                                          unsigned* prog, int& o_len, int2& o_end, bool& o_out) {
+//
+// Segmented traceback (pd.spec_every > 0).  A walk is one wave's chain of
+// dependent scalar steps, ~0.1 us per move on a busy chip: a 35k x 90k pair of
+// big13 took 7-11 ms, all of it after the pair's last band filled.  So every
+// band b but the last, once filled, traces a speculative segment of its own
+// rows (SPEC): from its last row at a guessed column up to the band's top,
+// recording for each row the cell it entered the row at and its move index
+// (recs, epoch-tagged).  Traceback paths from different cells merge and then
+// coincide (the walk is deterministic), so the pair's own walk (from (m, n),
+// on the wave that filled the last band) checks at each pass start whether its
+// cell lies on band b's segment -- row r's entry column c_hi and the row's L
+// moves give the segment's cells on r -- and on a hit copies the segment's
+// remaining moves and jumps to its exit: the walk then only crosses the rows
+// from a band's bottom to the merge.  A segment that fails (left the stored
+// window) is never merged into; a band whose segment never merges is walked
+// in full, as before.
+template <bool SPEC>
+__device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd, unsigned char* obuf, int lane, int sb,
+                                          int& o_len, int2& o_end, bool& o_out) {
   const int nblk = pd.bits_nblk, win = pd.bits_w;
   const int64_t bdw = (int64_t)nblk * 1024;  // dwords per band
   const unsigned* mat = a.mat + pd.mat_off;
-  uint8_t* ops = a.ops + pd.ops_off;
+  const bool segd = pd.spec_every > 0;
+  // segments (nwk_internal.h colseg_*): band b's records at recs + rec_off + b
+  // 2048, info at seginfo + 4 (seg_off + b), moves at segops + segops_off + b cap
+  u64* const srec = a.recs + pd.rec_off;
+  int* const sinfo = a.seginfo + 4 * pd.seg_off;
+  uint8_t* const smov = a.segops + pd.segops_off;
+  const int64_t scap = colseg_cap(pd.n);
+  const u64 ep20 = (u64)(a.epoch & 0xfffffu);
+  uint8_t* ops = SPEC ? smov + (int64_t)sb * scap : a.ops + pd.ops_off;
   const unsigned ob = (unsigned)(uintptr_t)obuf;
   int Lc = 0, flushed = 0;
   auto flush = [&](int upto) {
@@ -252,19 +396,81 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
     }
     flushed = upto;
   };
+  // (pair walk) append n moves from src (a finished segment) to ops at Lc:
+  // head bytes to a dword boundary, dwords (two aligned source dwords and
+  // v_alignbyte each), tail bytes; the ring gets the bytes of the last partial
+  // dword, which the next flush rewrites
+  auto seg_copy = [&](const uint8_t* src, int n) {
+    flush(Lc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int d0 = Lc;
+    const int h = smin(n, (4 - (d0 & 3)) & 3);
+    if (lane < h) ops[d0 + lane] = src[lane];
+    const int nd = (n - h) >> 2;
+    const uintptr_t sa = (uintptr_t)(src + h);
+    const unsigned* s0 = reinterpret_cast<const unsigned*>(sa & ~(uintptr_t)3);
+    const unsigned sh = (unsigned)(sa & 3);
+    unsigned* dw = reinterpret_cast<unsigned*>(ops + d0 + h);
+    for (int w0 = 0; w0 < nd; w0 += 256) {
+      unsigned lo[4], hi[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int w = w0 + 64 * k + lane;
+        lo[k] = w < nd ? s0[w] : 0u;
+        hi[k] = w < nd ? s0[w + 1] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int w = w0 + 64 * k + lane;
+        if (w < nd) dw[w] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh);
+      }
+    }
+    const int t = (n - h) & 3;
+    if (lane < t) ops[d0 + h + 4 * nd + lane] = src[h + 4 * nd + lane];
+    const int e = d0 + n, e0 = e & ~3;
+    if (lane < e - e0 && e0 + lane >= d0)
+      asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((e0 + lane) & (kTraceRing - 1))), "v"((unsigned)src[e0 + lane - d0])
+                   : "memory");
+    Lc = e;
+    flushed = e;
+  };
   int b = (pd.m - 1) / kBR, r = (pd.m - 1) % kBR, c = pd.n - 1;
+  if constexpr (SPEC) {  // band sb's last row, at the proportional diagonal's column
+    b = sb;
+    r = kBR - 1;
+    c = (int)(((int64_t)(sb + 1) * kBR - 1) * pd.n / pd.m);
+    c = c > pd.n - 1 ? pd.n - 1 : c;
+  }
   if (a.dbg_notrace) c = -1;  // NWK_NOTRACE (fill timing): no moves
   int tb = -1, blo = 0, slo = 0;
   const int64_t lim = (int64_t)win * pd.m;
   if (win > 0 && c >= 0) {  // the walk's first cell
-    const int64_t dev = (int64_t)c * pd.m - (int64_t)(pd.m - 1) * pd.n;
+    const int64_t dev = (int64_t)c * pd.m - ((int64_t)b * kBR + r) * pd.n;
     if (dev > lim || dev < -lim) c = -2;  // (out below)
   }
+  if (SPEC && c >= 0 && lane == 0)  // the segment's first cell: row kBR - 1, move 0
+    __hip_atomic_store(srec + (int64_t)sb * kBR + kBR - 1, (ep20 << 44) | ((u64)c << 22), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   bool bad = false, out = false;
-  // one tile ahead: anchored 64 columns on at the row-lane the walk is
-  // predicted to enter it (rows per column ~ m / n), 24 rows of slack above
-  unsigned nd[4] = {0, 0, 0, 0}, nu[4] = {0, 0, 0, 0};
-  int ncts = -1, nta = -1, nb_ = -1;
+  int nomerge = -1;  // a band whose segment failed
+  unsigned n_merge = 0;
+  // The current tile (cts, tta: columns cts - 63 .. cts, row-lanes tta - 3 ..
+  // tta of band ctb) stays while the walk is inside it -- a pass that runs off
+  // its key window only re-windows -- and one tile ahead is in flight: where
+  // the walk is predicted to leave the current one (rows per column ~ m / n),
+  // through its left edge (64 columns on, 24 rows of slack above the entry
+  // row) or its top (the row-lanes above, 16 columns of slack to the right).
+  unsigned vd[4] = {0, 0, 0, 0}, vu[4] = {0, 0, 0, 0}, nd[4] = {0, 0, 0, 0}, nu[4] = {0, 0, 0, 0};
+  int cts = -1, tta = -1, ctb = -1, ncts = -1, nta = -1, nb_ = -1;
+  // (pair walk) band bb's segment records of the tile's 128 rows, two per lane
+  u64 rq[2] = {0, 0}, nrq[2] = {0, 0};
+  auto recs_on = [&](int bb) { return !SPEC && segd && bb < pd.nbands - 1 && bb != nomerge; };
+  auto load_recs = [&](int bb, int ta_, u64 (&q)[2]) {
+    const int row = (ta_ > 3 ? 32 * (ta_ - 3) : 0) + 2 * lane;
+    const u64* p = srec + (int64_t)bb * kBR + row;
+    q[0] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    q[1] = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
   auto load_tile = [&](int bb, int blo_, int cts_, int ta_, unsigned (&d)[4], unsigned (&u)[4]) {
     const int cl = cts_ - lane;
 #pragma unroll
@@ -280,12 +486,20 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
       u[k] = __builtin_nontemporal_load(p + 512);
     }
   };
+  auto rowlo_of = [](int ta_) { return ta_ > 3 ? 32 * (ta_ - 3) : 0; };
   const int64_t rpc = ((int64_t)pd.m << 16) / pd.n;  // rows per column (16.16)
+  // key window base below the entry key: wide pairs' walks climb keys (L
+  // moves, +1), tall pairs' descend (U moves, -1)
+  const int kback = rpc < 52429 ? 4 : (rpc > 81920 ? 28 : 16);
   const u64 tc0 = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
   unsigned n_tiles = 0, n_dem = 0, n_stops = 0;
+#if NWK_TRACE_PROF  // (A/B build: cycles per phase, printed per pair)
+  u64 p_sw = 0, p_wait = 0, p_win = 0, p_walk = 0, p_out = 0, n_pass = 0;
+#endif
   if (c == -2) out = true;
   while (!out && c >= 0 && (b > 0 || r >= 0)) {
     if (r < 0) {  // into the band above
+      if constexpr (SPEC) break;  // (a segment ends at its band's top)
       --b;
       r += kBR;
     }
@@ -302,45 +516,130 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
         break;
       }
     }
-    if (Lc - flushed >= kTraceRing - 256) flush(Lc & ~3);  // (a tile adds <= 64 + 128 moves)
-    const int rowlo = ta > 3 ? 32 * (ta - 3) : 0;
-    // the tile: the prefetched one when the walk entered it, else loaded now
-    int cts, tta;
-    unsigned vd[4], vu[4];
-    if (nb_ == b && c <= ncts && c > ncts - 32 && ta <= nta && ta >= nta - 2) {
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-      cts = ncts;
-      tta = nta;
+#if NWK_TRACE_PROF
+    const u64 pt0 = __builtin_amdgcn_s_memtime();
+#endif
+    if (Lc - flushed >= kTraceRing - 256) flush(Lc & ~3);  // (a pass adds <= 64 + 128 moves)
+    if (!(ctb == b && c > cts - 64 && ta <= tta && r >= rowlo_of(tta))) {
+      if (nb_ == b && c <= ncts && c > ncts - 64 && ta <= nta && r >= rowlo_of(nta)) {  // the tile ahead
+#if NWK_TRACE_PROF
+        const u64 pw0 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+        p_wait += __builtin_amdgcn_s_memtime() - pw0;
+#endif
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+        cts = ncts;
+        tta = nta;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        vd[k] = nd[k];
-        vu[k] = nu[k];
-      }
-    } else {
-      ++n_dem;
-      cts = c;
-      tta = ta;
-      load_tile(b, blo, cts, tta, vd, vu);
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-    }
-    ++n_tiles;
-    const int trowlo = tta > 3 ? 32 * (tta - 3) : 0;
-    // prefetch the tile after this one
-    {
-      const int c2 = cts - 64;
-      const int rp = r - (int)(((int64_t)(cts - c + 64) * rpc) >> 16);
-      if (c2 >= slo && rp >= 24) {
-        nb_ = b;
-        ncts = c2;
-        int pa = (rp + 24) >> 5;
-        pa = pa > kBR / 32 - 1 ? kBR / 32 - 1 : pa;
-        nta = __builtin_amdgcn_readfirstlane(pa);
-        load_tile(b, blo, ncts, nta, nd, nu);
+        for (int k = 0; k < 4; ++k) {
+          vd[k] = nd[k];
+          vu[k] = nu[k];
+        }
+        rq[0] = nrq[0];
+        rq[1] = nrq[1];
       } else {
-        nb_ = -1;
+        ++n_dem;
+        cts = c;
+        tta = ta;
+        load_tile(b, blo, cts, tta, vd, vu);
+        if (recs_on(b)) load_recs(b, tta, rq);
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+      }
+      ctb = b;
+      ++n_tiles;
+      // the tile after this one
+      const int tlo = rowlo_of(tta);
+      const int64_t cl = c - (cts - 64);          // columns to the left edge
+      const int64_t rt = r - tlo + 1;             // rows to the top
+      nb_ = -1;
+      if (tlo > 0 && (rt << 16) < cl * rpc) {     // leaves through the top
+        const int ce = c - (int)((rt << 16) / (rpc > 0 ? rpc : 1));
+        const int c2 = smin(cts, ce + 16);
+        if (c2 >= slo) {
+          nb_ = b;
+          ncts = __builtin_amdgcn_readfirstlane(c2);
+          nta = __builtin_amdgcn_readfirstlane((tlo >> 5) - 1);
+        }
+      } else {                                    // through the left edge
+        const int c2 = cts - 64;
+        const int rp = r - (int)((cl * rpc) >> 16);
+        if (c2 >= slo && rp >= 0) {
+          nb_ = b;
+          ncts = c2;
+          int pa = (rp + 24) >> 5;
+          pa = pa > kBR / 32 - 1 ? kBR / 32 - 1 : pa;
+          nta = __builtin_amdgcn_readfirstlane(pa);
+        }
+      }
+      if (nb_ >= 0) {
+        load_tile(b, blo, ncts, nta, nd, nu);
+        if (recs_on(b)) load_recs(b, nta, nrq);
       }
     }
-    (void)rowlo;
+    const int trowlo = rowlo_of(tta);
+    // (pair walk) is this cell on band b's segment?  Row r's record: the entry
+    // column c_hi and move index k; row r - 1's index gives the row's L moves,
+    // so its cells are c_hi - nL .. c_hi
+    if (recs_on(b)) {
+      const int ix = r - trowlo;  // 0 .. 127
+      auto rec_at = [&](int x) {
+        const u64 v = (x & 1) ? rq[1] : rq[0];
+        const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, x >> 1);
+        const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), x >> 1);
+        return ((u64)hi << 32) | lo;
+      };
+      const u64 e = rec_at(ix);
+      int kk = -1;
+      if ((e >> 44) == ep20) {
+        const int chi = (int)((e >> 22) & 0x3fffffu), khi = (int)(e & 0x3fffffu);
+        if (c == chi) {
+          kk = khi;
+        } else if (c < chi && ix > 0) {
+          const u64 e1 = rec_at(ix - 1);
+          if ((e1 >> 44) == ep20 && c >= chi - ((int)(e1 & 0x3fffffu) - khi - 1)) kk = khi + (chi - c);
+        }
+      }
+      if (kk >= 0) {
+        // merged: wait for the segment to finish, then its moves kk .. len - 1
+        int* inf = sinfo + 4 * b;
+        for (;;) {
+          const unsigned f = __builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)inf, BITS_RLX));
+          if (f == a.epoch) break;
+          if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)a.err, BITS_RLX)) != 0u) {
+            bad = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (bad) break;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const int slen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(inf + 1, BITS_RLX));
+        const int xi = __builtin_amdgcn_readfirstlane(__hip_atomic_load(inf + 2, BITS_RLX));
+        const int xc = __builtin_amdgcn_readfirstlane(__hip_atomic_load(inf + 3, BITS_RLX));
+        if (slen < 0 || kk > slen) {
+          nomerge = b;  // (failed segment: walk the band)
+        } else {
+          seg_copy(smov + (int64_t)b * scap + kk, slen - kk);
+          ++n_merge;
+          b = xi >= 0 ? xi / kBR : -1;
+          r = xi - b * kBR;
+          if (xi < 0) {  // the segment reached row -1 (band 0's top)
+            b = 0;
+            r = -1;
+          }
+          c = xc;
+          if (Lc > pd.m + pd.n) {
+            bad = true;
+            break;
+          }
+          continue;
+        }
+      }
+    }
+#if NWK_TRACE_PROF
+    const u64 pt1 = __builtin_amdgcn_s_memtime();
+    p_sw += pt1 - pt0;
+#endif
     const int LL = smin(63, cts - slo);  // last lane whose column is >= the lowest stored step
     int L = cts - c;
     int K = r + L;
@@ -355,7 +654,7 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
       const int64_t dev = (int64_t)(cts - Ll) * pd.m - (ib + Kk - Ll) * pd.n;
       return dev > lim || dev < -lim;
     };
-    const int Kb = K - 16;
+    const int Kb = K - kback;
     // key window: lane l's bit i = its cell at row Kb + i - l: bit q of the
     // column {0, vd[3], vd[2], vd[1], vd[0], 0} (rows below / above the tile read 0)
     unsigned WD, WU;
@@ -370,74 +669,127 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
       WD = ok ? __builtin_amdgcn_alignbit(dhi, dlo, sh) : 0u;
       WU = ok ? __builtin_amdgcn_alignbit(uhi, ulo, sh) : ~0u;  // stored up word: 0 = UP
     }
+    const unsigned WL = WU & ~WD;  // cells that move L: neither D nor U
+#if NWK_TRACE_PROF
+    const u64 pt2 = __builtin_amdgcn_s_memtime();
+    p_win += pt2 - pt1;
+#endif
     const int L0 = L;
     u64 finL = 0;          // lanes whose last move is L
     unsigned nUv = 0;      // per lane: U moves (written by v_writelane)
     int maxU = 0;
-    int Kc = -(1 << 30);
-    u64 Dm = 0, Um = 0;
-    for (;;) {
-      const int bnd = smin(K - trowlo, LL);
-      if (L > bnd) break;  // the cell is below the tile's rows or past its columns
-      const int i = K - Kb;
-      if ((unsigned)i > 31u) break;  // off the key window: a new tile here
-      if (wchk && outside(L, K)) {
-        out = true;
-        break;
+    // a horizontal run: after an L move the walk stays on row rr = K - L; one
+    // ballot of the row's cells (lane l's key-window bit rr - Kb + l) that move
+    // L takes the whole run to the first lane that moves D or U (or to the edge
+    // of the readable cells) -- wide pairs' paths are mostly long L runs
+    // (big13 35k x 90k: 55k L moves of 90k), one loop trip each before.
+    // False: the run's last cell is outside the stored window.
+    auto lrun = [&](auto chk_t) -> bool {
+      constexpr bool CHK = decltype(chk_t)::value;
+      const int rr = K - L;
+      const int lend_r = smin(LL, 31 + Kb - rr) + 1;  // first lane whose row-rr cell is not readable
+      if (L >= lend_r) return true;
+      // (lanes whose bit rr - Kb + l is off the window are past lend_r: v_bfe's
+      // offset wraps there, and the min below discards them)
+      const u64 Lm = __builtin_amdgcn_ballot_w64(__builtin_amdgcn_ubfe(WL, (unsigned)(rr - Kb + lane), 1u) != 0u);
+      const int le = sminu(sff1u(~Lm & (~0ull << L)), lend_r);
+      if (le == L) return true;
+      if constexpr (CHK) {
+        if (outside(le - 1, rr + le - 1)) return false;
       }
-      if (K != Kc) {
-        Dm = __builtin_amdgcn_ballot_w64((WD >> i) & 1u);
-        Um = __builtin_amdgcn_ballot_w64(!((WU >> i) & 1u));
-        Kc = K;
-      }
-      const int lend = bnd + 1;  // first lane past the readable cells of this key
-      const u64 stops = ~Dm & (~0ull << L);
-      const int ls = sminu(sff1u(stops), lend);  // (no stop: ff1 = -1)
-      if (wchk && outside(ls < lend ? ls : lend - 1, K)) {  // the run's last cell read
-        out = true;
-        break;
-      }
-      if (ls >= lend) {  // D moves through lanes L .. lend - 1
-        L = lend;
-        break;
-      }
-      ++n_stops;
-      if ((Um >> ls) & 1ull) {
-        // a U move, then down lane ls's column: U while D is clear and U set
-        const unsigned wd = (unsigned)__builtin_amdgcn_readlane((int)WD, ls);
-        const unsigned wu = (unsigned)__builtin_amdgcn_readlane((int)WU, ls);
-        const int jlo = smax(trowlo + ls - Kb, 0);  // lowest key bit inside the tile's rows
-        const unsigned below = i >= 31 ? ~0u : ((2u << i) - 1u);
-        const unsigned stopm = (wd | wu) & below & ~((1u << jlo) - 1u);
-        if (wchk && outside(ls, Kb + (stopm ? 31 - __builtin_clz(stopm) : jlo))) {  // the vertical run's last cell
+      finL |= (le >= 64 ? ~0ull : ((1ull << le) - 1ull)) & (~0ull << L);
+      L = le;
+      K = rr + le;
+      return true;
+    };
+    // The run loop, all scalar; the CHK copy checks the stored lane words
+    // (windowed storage, only in tiles near the window's edge).
+    auto walk = [&](auto chk_t) {
+      constexpr bool CHK = decltype(chk_t)::value;
+      for (;;) {
+        const int bnd = smin(K - trowlo, LL);
+        if (L > bnd) break;  // the cell is below the tile's rows or past its columns
+        const int i = K - Kb;
+        if ((unsigned)i > 31u) break;  // off the key window: re-window
+        if constexpr (CHK) {
+          if (outside(L, K)) {
+            out = true;
+            break;
+          }
+        }
+        // (every stop changes the key: the key's lane masks are built each trip)
+        const u64 Dm = __builtin_amdgcn_ballot_w64(__builtin_amdgcn_ubfe(WD, (unsigned)i, 1u) != 0u);
+        const u64 Um = __builtin_amdgcn_ballot_w64(__builtin_amdgcn_ubfe(WU, (unsigned)i, 1u) == 0u);
+        const int lend = bnd + 1;  // first lane past the readable cells of this key
+        const u64 stops = ~Dm & (~0ull << L);
+        const int ls = sminu(sff1u(stops), lend);  // (no stop: ff1 = -1)
+        if constexpr (CHK) {
+          if (outside(ls < lend ? ls : lend - 1, K)) {  // the run's last cell read
+            out = true;
+            break;
+          }
+        }
+        if (ls >= lend) {  // D moves through lanes L .. lend - 1
+          L = lend;
+          break;
+        }
+        if ((Um >> ls) & 1ull) {
+          // a U move, then down lane ls's column: U while D is clear and U set
+          const unsigned wd = (unsigned)__builtin_amdgcn_readlane((int)WD, ls);
+          const unsigned wu = (unsigned)__builtin_amdgcn_readlane((int)WU, ls);
+          const int jlo = smax(trowlo + ls - Kb, 0);  // lowest key bit inside the tile's rows
+          const unsigned below = i >= 31 ? ~0u : ((2u << i) - 1u);
+          const unsigned stopm = (wd | wu) & below & ~((1u << jlo) - 1u);
+          if constexpr (CHK) {
+            if (outside(ls, Kb + (stopm ? 31 - __builtin_clz(stopm) : jlo))) {  // the vertical run's last cell
+              out = true;
+              break;
+            }
+          }
+          if (stopm == 0u) {  // the run leaves the tile's rows (or the key window): U moves down to there
+            const int nU = i - jlo + 1;
+            nUv = writelane(nUv, nU, ls);
+            maxU = nU > maxU ? nU : maxU;
+            L = ls;
+            K = Kb + jlo - 1;
+            break;
+          }
+          const int j = 31 - __builtin_clz(stopm);
+          const int nU = i - j;
+          nUv = writelane(nUv, nU, ls);
+          maxU = nU > maxU ? nU : maxU;
+          L = ls + 1;
+          if ((wd >> j) & 1u) {  // the cell at key j moves D
+            K = Kb + j;
+            continue;
+          }
+          finL |= 1ull << ls;  // ... or L
+          K = Kb + j + 1;
+        } else {  // an L move
+          finL |= 1ull << ls;
+          L = ls + 1;
+          K = K + 1;
+        }
+        if (!lrun(chk_t)) {
           out = true;
           break;
         }
-        if (stopm == 0u) {  // the run leaves the tile's rows (or the key window): U moves down to there
-          const int nU = i - jlo + 1;
-          nUv = writelane(nUv, nU, ls);
-          maxU = nU > maxU ? nU : maxU;
-          L = ls;
-          K = Kb + jlo - 1;
-          break;
-        }
-        const int j = 31 - __builtin_clz(stopm);
-        const int nU = i - j;
-        nUv = writelane(nUv, nU, ls);
-        maxU = nU > maxU ? nU : maxU;
-        if ((wd >> j) & 1u) {  // the cell at key j moves D
-          K = Kb + j;
-        } else {  // ... or L
-          finL |= 1ull << ls;
-          K = Kb + j + 1;
-        }
-        L = ls + 1;
-      } else {  // an L move
-        finL |= 1ull << ls;
-        L = ls + 1;
-        K = K + 1;
       }
+    };
+    if (wchk) {
+      walk(std::true_type{});
+    } else {
+#if NWK_COL_CWALK  // (A/B: the compiled walk)
+      walk(std::false_type{});
+#else
+      walk_asm(WD, WU, WL, lane, Kb, trowlo, LL, K, L, finL, nUv, maxU);
+#endif
     }
+#if NWK_TRACE_PROF
+    const u64 pt3 = __builtin_amdgcn_s_memtime();
+    p_walk += pt3 - pt2;
+    ++n_pass;
+#endif
     // the tile's moves in walk order: lanes L0 .. L - 1 are done (U^nU, then D
     // or L), lane L (when <= 63) holds only its U moves so far
     {
@@ -457,14 +809,53 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
         asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((Lc + (int)(off + nU)) & (kTraceRing - 1))), "v"(ch)
                      : "memory");
       }
+      if constexpr (SPEC) {
+        // the rows this pass entered: lane l's U moves enter rows r0 - 1 .. r0 - nU
+        // at its column, its D move row r0 - nU - 1 at the next; r0 = the pass's
+        // row minus the rows of the lanes before (exclusive scan of nU + D)
+        const bool isD = fin && !((finL >> lane) & 1ull);
+        const unsigned dr = nU + (isD ? 1u : 0u);
+        const int r0 = r - (int)(shadev::wave_incl_scan(dr, lane) - dr);
+        const int col = cts - lane;
+        u64* rb = srec + (int64_t)sb * kBR;
+        for (int j = 1; j <= maxU + 1; ++j) {
+          const bool u = (unsigned)j <= nU, d = isD && (unsigned)j == nU + 1;
+          const int rr = r0 - j;
+          if ((u || d) && rr >= 0) {
+            const int cc = d ? col - 1 : col;
+            const u64 k = (u64)(Lc + (int)off + j);
+            if (cc >= 0)
+              __hip_atomic_store(rb + rr, (ep20 << 44) | ((u64)cc << 22) | k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
       Lc += (int)tot;
+      if (a.stamps) n_stops += (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64(fin && ((finL >> lane) & 1ull || nU)));
     }
     r = K - L;
     c = cts - L;
+#if NWK_TRACE_PROF
+    p_out += __builtin_amdgcn_s_memtime() - pt3;
+#endif
     if (Lc > pd.m + pd.n) {
       bad = true;
       break;
     }
+  }
+  if constexpr (SPEC) {
+    // the segment: its moves, then {length (-1: failed), exit cell} and the flag
+    flush(Lc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      int* inf = sinfo + 4 * sb;
+      __hip_atomic_store(inf + 1, (out || bad) ? -1 : Lc, BITS_RLX);
+      __hip_atomic_store(inf + 2, b * kBR + r, BITS_RLX);
+      __hip_atomic_store(inf + 3, c, BITS_RLX);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (lane == 0) __hip_atomic_store((gu32*)(sinfo + 4 * sb), a.epoch, BITS_RLX);
+    return;
   }
   if (bad && lane == 0) atomicOr(a.err, 16u);
   if (a.stamps && lane == 0) {
@@ -472,10 +863,16 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
     x[2] = __builtin_amdgcn_s_memtime() - tc0;
     x[3] = n_stops;
     x[4] = (u64)Lc;
-    x[5] = ((u64)n_tiles << 32) | ((u64)n_dem << 16);
+    x[5] = ((u64)n_tiles << 32) | ((u64)n_dem << 16) | (u64)(n_merge & 0xffffu);
   }
   flush(Lc);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if NWK_TRACE_PROF
+  if (lane == 0)
+    printf("trace_col %d x %d: moves %d passes %llu tiles %u demand %u | cycles switch %llu (wait %llu) window %llu walk %llu out %llu\n",
+           pd.m, pd.n, Lc, (unsigned long long)n_pass, n_tiles, n_dem, (unsigned long long)p_sw, (unsigned long long)p_wait,
+           (unsigned long long)p_win, (unsigned long long)p_walk, (unsigned long long)p_out);
+#endif
   o_len = out ? 0 : Lc;
   o_end = (a.dbg_notrace || out) ? make_int2(pd.m, pd.n) : make_int2(b * kBR + r + 1, c + 1);
   o_out = out;
@@ -484,7 +881,6 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
     a.endij[pd.slot] = o_end;
     if (out) a.retry[pd.slot] = 1;
   }
-  (void)prog;
 }
 
 // Waves per SIMD the kernel is compiled for (NWK_COL_WPE; register budget 512 / WPE)
@@ -664,7 +1060,7 @@ __global__ __launch_bounds__(256) NWK_COL_OCC void nw_align_col(FillArgs a) {
 #if !defined(NWK_COL_TRACE_PRIO) || NWK_COL_TRACE_PRIO
       __builtin_amdgcn_s_setprio(3);
 #endif
-      trace_col(a, pd, obuf_all[wid], lane, prog, tlen, tend, tout);
+      trace_col<false>(a, pd, obuf_all[wid], lane, 0, tlen, tend, tout);
       __builtin_amdgcn_s_setprio(0);
       if constexpr (FUSE) {
         const bool ok_rows = !tout && fin_rows(a, pd, lane, tlen, tend);
@@ -672,6 +1068,13 @@ __global__ __launch_bounds__(256) NWK_COL_OCC void nw_align_col(FillArgs a) {
       }
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
       BITS_PROG(0x56000000u);
+    } else if (pd.spec_every > 0 && band + 1 < pd.nbands) {  // segmented: this band's speculative segment
+      int tlen;
+      int2 tend;
+      bool tout;
+      __builtin_amdgcn_s_setprio(3);
+      trace_col<true>(a, pd, obuf_all[wid], lane, band, tlen, tend, tout);
+      __builtin_amdgcn_s_setprio(0);
     }
   }
 }

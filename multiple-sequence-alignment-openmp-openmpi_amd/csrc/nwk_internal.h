@@ -84,6 +84,17 @@ __host__ __device__ inline int bits_blk_lo(int b, int m, int n, int w) {
 // word of a stored block holds such a cell, so all are written
 __host__ __device__ inline bool bits_lane_window(int w) { return w > 0 && w < kBitsRows; }
 
+// kCol segmented traceback (PairDesc::spec_every > 0; nwk_col.hip trace_col):
+// for each band b < nbands - 1 of a pair, its speculative segment's
+//   records  u64 [2048] at recs + rec_off + 2048 b: row rr's entry cell
+//            {epoch & 0xfffff : 20 | column : 22 | move index : 22}
+//   info     int4 at seginfo + 4 (seg_off + b): {flag = epoch once done,
+//            length (-1: failed), exit row (absolute), exit column}
+//   moves    u8 [colseg_cap(n)] at segops + segops_off + b cap
+__host__ __device__ inline int64_t colseg_cap(int n) { return ((int64_t)kBitsRows + n + 64 + 16 + 127) / 128 * 128; }
+// record fields: 22-bit column and move index (a band's segment has < 2048 + n + 64 moves)
+__host__ __device__ inline bool colseg_ok(int n) { return (int64_t)kBitsRows + n + 64 < (1 << 22); }
+
 // kBitsStrip: first stored 8-step block (strip step numbering) of band b's
 // window: its cells (i, j), |j - i n / m| <= w, sit at steps j + b np + (i - 2048 b)
 __host__ __device__ inline int strip_blk_lo(int b, int m, int n, int np, int w) {

@@ -171,7 +171,10 @@ struct nwk_ctx {
   DevBuf d_work;                // matrices | boundary granules | op strings
   int64_t clean_b = 0;          // leading bytes of d_work holding only zeros / old-epoch granules
   DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij, d_done, d_stamps, d_prog, d_retry;
-  DevBuf d_segctl;              // kPacked2: task-done flags | segment info | traceback records
+  DevBuf d_segctl;              // kPacked2: task-done flags | segment info | traceback records; kCol: segment records
+  DevBuf d_colinfo;             // kCol: segment info (int4 per segment), cleared per batch
+  int64_t colseg_clean_b = 0;   // kCol: leading bytes of d_segctl holding only zeros / kCol records of older epochs
+  unsigned colseg_epoch0 = 0;   // kCol: the epoch of the last clear (records' tags wrap after 2^20 launches)
   DevBuf d_pen, d_hash;         // device finalize (nw_hash): per pair penalty, problemhash
   DevBuf d_hq;                  // fused finalize: queue of traced pairs | row lengths and penalties
   DevBuf d_msa[3];              // nwk_msa: row profiles | column profiles | granules, matrices, moves
@@ -229,7 +232,7 @@ void nwk_ctx_destroy(nwk_ctx* c) {
   c->d_pairs.release(); c->d_tasks.release(); c->d_ctl.release();
   c->d_oplen.release(); c->d_endij.release(); c->d_done.release(); c->d_stamps.release(); c->d_retry.release();
   c->h_retry.release();
-  c->d_segctl.release(); c->d_prog.release(); c->d_pen.release(); c->d_hash.release(); c->d_hq.release();
+  c->d_segctl.release(); c->d_colinfo.release(); c->d_prog.release(); c->d_pen.release(); c->d_hash.release(); c->d_hq.release();
   for (auto& b : c->d_msa) b.release();
   for (int b = 0; b < 2; ++b) { c->h_pen[b].release(); c->h_hash[b].release(); c->h_rec[b].release(); }
   c->h_tasks.release();
@@ -638,8 +641,16 @@ void footprint(PairWork* w, int bits, int mode, bool affine) {
   }
   if (mode == kCol) {
     const int64_t nb = ceil_div(w->m, kBitsRows), nw = ceil_div(w->n, 32);
-    w->segops_b = w->segctl_b = 0;
-    w->spec = 0;
+    // segmented traceback (nwk_col.hip trace_col): a speculative segment per
+    // band but the last -- move buffers in segops, records and segment info in
+    // the control buffer.  NWK_COL_SEG=0: whole-pair walks only.
+    static const int seg_env = getenv("NWK_COL_SEG") ? atoi(getenv("NWK_COL_SEG")) : 1;
+    const bool seg = seg_env != 0 && nb >= 2 && colseg_ok(w->n);
+    w->spec = seg ? 1 : 0;
+    w->nguess = 1;
+    w->njobs = 0;
+    w->segops_b = seg ? (nb - 1) * colseg_cap(w->n) : 0;
+    w->segctl_b = seg ? (nb - 1) * ((int64_t)kBitsRows * 8 + 16) : 0;
     w->bits_nblk = (int)col_nblk_of(w->m, w->n, w->bits_w);
     w->mat_dw = nb * w->bits_nblk * 1024;
     w->bnd_gr = (nb - 1) * nw * 4;  // NP <= 4 granules per 32 columns of each band's last row
@@ -1141,8 +1152,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   if ((bitsy || pl.mode == kAffinePk) && !dp.empty() && win_env != 0) {
     auto total_b = [&]() {
       int64_t mat = 0, bnd = 0, ops = 0;
-      for (const auto& w : dp) mat += w.mat_dw, bnd += w.bnd_gr, ops += w.ops_b;
-      return mat * 4 + bnd * 8 + 3 * ops + 8192;
+      int64_t seg = 0;
+      for (const auto& w : dp) mat += w.mat_dw, bnd += w.bnd_gr, ops += w.ops_b, seg += w.segops_b + w.segctl_b;
+      return mat * 4 + bnd * 8 + 3 * ops + seg + 8192;
     };
     auto set_w = [&](int W) {
       for (auto& w : dp) {
@@ -1174,8 +1186,26 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     // profiles/r02/pathdev_*.txt), at least 1024 and at most a budget-forced W.
     // A path that strays further re-runs with full storage.  NWK_COL_WIN:
     // 0 = full storage when it fits, W > 0 forced.
+    //
+    // Only a job whose full storage would be written faster than ~4 TB/s takes
+    // it: estimated fill time max(cells / 32k GCUPS, longest pair span x 0.3 us
+    // per wave-step under load), span = n + 100 per band.  A job bound by one
+    // long pair's span (big13: 94k steps) writes ~2.5 TB/s in full and keeps
+    // full storage -- related sequences' paths stray far from the diagonal
+    // (big13: 2.9k-50k columns, profiles/r04/pathdev_big13.txt), so a window
+    // there sends nearly every pair to the re-run.
     static const int col_win_env = getenv("NWK_COL_WIN") ? atoi(getenv("NWK_COL_WIN")) : -1;
-    if (pl.mode == kCol && win_env < 0 && col_win_env != 0) {
+    bool col_wb = col_win_env > 0;
+    if (pl.mode == kCol && col_win_env < 0) {
+      double cells = 0, bytes = 0, span = 0;
+      for (const auto& w : dp) {
+        cells += (double)w.m * w.n;
+        bytes += (double)w.m * w.n / 4;
+        span = std::max(span, (double)w.n + 100.0 * (double)ceil_div(w.m, kBitsRows));
+      }
+      col_wb = bytes / std::max(cells / 3.2e13, span * 3.0e-7) > 4e12;
+    }
+    if (pl.mode == kCol && win_env < 0 && col_wb) {
       for (auto& w : dp) {
         const double est = 400.0 * std::pow(std::max(w.m, w.n) / 8000.0, 2.0 / 3.0);
         int wc = col_win_env > 0 ? col_win_env : (int)round_up(std::max<int64_t>(1024, (int64_t)(2.5 * est)), 256);
@@ -1261,10 +1291,11 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     // ---- form a batch that fits the HBM budget
     size_t end = pos;
     bool lin_one = false;
-    int64_t mat = 0, bnd = 0, ops = 0, segops = 0;
+    int64_t mat = 0, bnd = 0, ops = 0, segops = 0, segctl = 0;
     while (end < dp.size()) {
       const PairWork& w = dp[end];
-      const int64_t need = (mat + w.mat_dw) * 4 + (bnd + w.bnd_gr) * 8 + 3 * (ops + w.ops_b) + segops + w.segops_b + 8192;
+      const int64_t need = (mat + w.mat_dw) * 4 + (bnd + w.bnd_gr) * 8 + 3 * (ops + w.ops_b) + segops + w.segops_b +
+                           segctl + w.segctl_b + 8192;
       if ((need > c->budget || lin_all) && end > pos) break;
       if (need > c->budget || lin_all) {  // a pair whose matrix does not fit: linear-space traceback (f2)
         if (c->opts.linear_space < 0 || sc.affine)
@@ -1273,7 +1304,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         lin_one = true;
         break;
       }
-      mat += w.mat_dw; bnd += w.bnd_gr; ops += w.ops_b; segops += w.segops_b;
+      mat += w.mat_dw; bnd += w.bnd_gr; ops += w.ops_b; segops += w.segops_b; segctl += w.segctl_b;
       ++end;
     }
     if (lin_one) {
@@ -1375,12 +1406,18 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       d.spec_every = w.spec;
       d.nguess = w.nguess;
       d.task_off = ntasks;  // one tdone entry per task
-      d.seg_off = nsegs;    // nguess seginfo entries per task
-      nsegs += tasks_of(pl.mode, d.nbands) * w.nguess;
-      njobs += w.njobs;
+      d.seg_off = nsegs;    // nguess seginfo entries per task (kCol: one per band but the last)
       d.rec_off = ro;
       d.segops_off = so;
-      ro += 32 * (w.m / 128 + 1);
+      if (pl.mode == kCol) {
+        const int64_t nseg = w.spec > 0 ? d.nbands - 1 : 0;
+        nsegs += nseg;
+        ro += nseg * kBitsRows;  // a record per row of each segment's band
+      } else {
+        nsegs += tasks_of(pl.mode, d.nbands) * w.nguess;
+        ro += 32 * (w.m / 128 + 1);
+      }
+      njobs += w.njobs;
       so += w.segops_b;
       mo += w.mat_dw; bo += w.bnd_gr; oo += w.ops_b;
       ntasks += tasks_of(pl.mode, d.nbands);
@@ -1461,6 +1498,27 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     if (segmented(pl.mode)) {
       if ((rc = c->d_segctl.ensure((size_t)segctl_b)) != NWK_OK) return rc;
       HIP_TRY(hipMemsetAsync(c->d_segctl.p, 0, (size_t)segctl_b, c->stream));
+      c->colseg_clean_b = 0;
+    }
+    // kCol segments: records (u64) in d_segctl, info (int4) in d_colinfo.  A
+    // record counts only with this launch's epoch tag (20 bits), so the record
+    // buffer is cleared only where it may hold anything else: fresh or grown
+    // memory, another mode's data, or once every 2^20 launches (the tag wraps).
+    // The info is cleared per batch (its flag is a whole epoch).
+    const bool colseg = pl.mode == kCol && nsegs > 0;
+    const int64_t colseg_ctl_b = ro * 8;
+    if (colseg) {
+      if ((rc = c->d_colinfo.ensure((size_t)nsegs * 16)) != NWK_OK) return rc;
+      HIP_TRY(hipMemsetAsync(c->d_colinfo.p, 0, (size_t)nsegs * 16, c->stream));
+      void* const old_ctl = c->d_segctl.p;
+      if ((rc = c->d_segctl.ensure((size_t)colseg_ctl_b)) != NWK_OK) return rc;
+      if (c->d_segctl.p != old_ctl || c->epoch + 2u - c->colseg_epoch0 >= (1u << 20)) c->colseg_clean_b = 0;
+      if (c->colseg_clean_b == 0) c->colseg_epoch0 = c->epoch;
+      if (colseg_ctl_b > c->colseg_clean_b) {
+        HIP_TRY(hipMemsetAsync(c->d_segctl.as<uint8_t>() + c->colseg_clean_b, 0, (size_t)(colseg_ctl_b - c->colseg_clean_b),
+                               c->stream));
+        c->colseg_clean_b = colseg_ctl_b;
+      }
     }
 
     FillArgs fa{};
@@ -1508,6 +1566,10 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.tdone = seg ? c->d_segctl.as<unsigned>() : nullptr;
     fa.seginfo = seg ? reinterpret_cast<int*>(c->d_segctl.as<uint8_t>() + seginfo_base_b) : nullptr;
     fa.recs = seg ? reinterpret_cast<unsigned long long*>(c->d_segctl.as<uint8_t>() + rec_base_b) : nullptr;
+    if (colseg) {
+      fa.recs = c->d_segctl.as<unsigned long long>();
+      fa.seginfo = c->d_colinfo.as<int>();
+    }
     fa.tj_ready = seg ? reinterpret_cast<unsigned*>(c->d_segctl.as<uint8_t>() + tjr_base_b) : nullptr;
     fa.tj_head = seg ? reinterpret_cast<unsigned*>(c->d_segctl.as<uint8_t>() + tjc_base_b) : nullptr;
     fa.tj_tail = seg ? fa.tj_head + 1 : nullptr;
@@ -1789,7 +1851,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         w.bits_w = 0;
         footprint(&w, pl.bits, pl.mode, sc.affine);
         auto need = [](const PairWork& x) {
-          return x.mat_dw * 4 + x.bnd_gr * 8 + 3 * x.ops_b + x.segops_b + 8192;
+          return x.mat_dw * 4 + x.bnd_gr * 8 + 3 * x.ops_b + x.segops_b + x.segctl_b + 8192;
         };
         if (pl.mode == kAffinePk && need(w) > c->budget) {
           // the affine path has no linear-space fallback: re-run with the

@@ -136,6 +136,30 @@ print(json.dumps(out))
 """
 
 
+@pytest.mark.parametrize("seg", ["0", "1"])
+def test_col_segmented_traceback_on_off(seg):
+    """Segmented traceback (trace_col: a speculative segment per band but the
+    last, merged into by the pair's own walk) forced off (NWK_COL_SEG=0, whole
+    walks) and on, in a child: related many-band pairs whose segments merge,
+    swapped halves whose segments never meet the path, ragged last bands."""
+    r = random.Random(977)
+    base = bytes(r.choice(ACGT) for _ in range(9000))
+    genes = _mutants(r, base, 3, ACGT) + [base[:6100], base[2500:]]
+    P, Q = (bytes(r.choice(ACGT) for _ in range(3000)) for _ in range(2))
+    genes += [P + Q, Q + P]
+    env = dict(os.environ, NWK_COL_SEG=seg)
+    res = subprocess.run([sys.executable, "-c", _CHILD, os.path.dirname(seqalign.__file__), str(0)],
+                         input=json.dumps([g.hex() for g in genes]).encode(), env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
+    assert res.returncode == 0, res.stderr.decode()[-2000:]
+    out = json.loads(res.stdout.decode().strip().splitlines()[-1])
+    for (pxy, pgap), o in zip(((3, 2), (5, 1)), out):
+        assert o["mode"] == 10
+        _, opens, ohs = oracle.all_pairs(genes, pxy, pgap)
+        assert o["pen"] == opens
+        assert o["hs"] == ohs
+
+
 @pytest.mark.parametrize("win", ["auto", "48", "700", "3000"])
 def test_col_windowed_storage_and_full_rerun(win):
     """Windowed storage (NWK_BITS_WIN, read once per process: a child) with a

@@ -3,6 +3,7 @@ For pair (i, j): max over the alignment of |col - row * n / m| (row = x index).
 Affine workloads (c5) trace with their (go, ge).
 usage: python tools/pathdev.py [workload=c3] [npairs=16]"""
 import math
+import os
 import sys
 
 sys.path.insert(0, "multiple-sequence-alignment-openmp-openmpi_amd")
@@ -10,8 +11,13 @@ import seqalign, workloads  # noqa: E402
 
 wl = sys.argv[1] if len(sys.argv) > 1 else "c3"
 npairs = int(sys.argv[2]) if len(sys.argv) > 2 else 16
-desc, k, L, pxy, pgap, affine = workloads.SYNTH[wl]
-genes = workloads.synth(k, L)
+if wl == "big13":  # the reference's own input (testing3), all 78 pairs unless npairs given
+    pxy, pgap, genes = seqalign.parse_input(open(os.path.join(workloads.GOLDEN_DATA, "mseq-big13-example.txt"), "rb").read())
+    affine = None
+    npairs = int(sys.argv[2]) if len(sys.argv) > 2 else 78
+else:
+    desc, k, L, pxy, pgap, affine = workloads.SYNTH[wl]
+    genes = workloads.synth(k, L)
 with seqalign.Engine(device=0) as e:
     devs = []
     for p in range(npairs):
@@ -30,5 +36,5 @@ with seqalign.Engine(device=0) as e:
             if c2 != 95: col += 1
             worst = max(worst, abs(col - row * n / m))
         devs.append(int(worst))
-        print("pair", p, (i, j), "penalty", pen, "max |dev|", int(worst), flush=True)
+        print("pair", p, (i, j), (m, n), "penalty", pen, "max |dev|", int(worst), flush=True)
 print("max over pairs", max(devs), "sorted", sorted(devs))
