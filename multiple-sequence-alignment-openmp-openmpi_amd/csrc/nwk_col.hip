@@ -382,7 +382,9 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
   uint8_t* const smov = a.segops + pd.segops_off;
   const int64_t scap = colseg_cap(pd.n);
   const u64 ep20 = (u64)(a.epoch & 0xfffffu);
-  uint8_t* ops = SPEC ? smov + (int64_t)sb * scap : a.ops + pd.ops_off;
+  uint8_t* ops = SPEC                ? smov + (int64_t)sb * scap
+                 : a.ops_host ? a.ops_host + (pd.ops_off - a.ops_base)  // (streamed host finalize)
+                              : a.ops + pd.ops_off;
   const unsigned ob = (unsigned)(uintptr_t)obuf;
   int Lc = 0, flushed = 0;
   auto flush = [&](int upto) {
@@ -488,6 +490,7 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
   };
   auto rowlo_of = [](int ta_) { return ta_ > 3 ? 32 * (ta_ - 3) : 0; };
   const int64_t rpc = ((int64_t)pd.m << 16) / pd.n;  // rows per column (16.16)
+  const int64_t cpr = ((int64_t)pd.n << 16) / pd.m;  // columns per row (16.16; no 64-bit divide per tile)
   // key window base below the entry key: wide pairs' walks climb keys (L
   // moves, +1), tall pairs' descend (U moves, -1)
   const int kback = rpc < 52429 ? 4 : (rpc > 81920 ? 28 : 16);
@@ -553,7 +556,7 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
       const int64_t rt = r - tlo + 1;             // rows to the top
       nb_ = -1;
       if (tlo > 0 && (rt << 16) < cl * rpc) {     // leaves through the top
-        const int ce = c - (int)((rt << 16) / (rpc > 0 ? rpc : 1));
+        const int ce = c - (int)((rt * cpr) >> 16);
         const int c2 = smin(cts, ce + 16);
         if (c2 >= slo) {
           nb_ = b;
@@ -880,6 +883,17 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
     a.oplen[pd.slot] = o_len;
     a.endij[pd.slot] = o_end;
     if (out) a.retry[pd.slot] = 1;
+    if (a.host_rec) {
+      int* h = a.host_rec + 4 * pd.slot;
+      h[1] = out ? -1 : o_len;
+      h[2] = o_end.x;
+      h[3] = o_end.y;
+    }
+  }
+  if (a.host_rec) {  // the moves (host memory) and the record, then its flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __threadfence_system();
+    if (lane == 0) __hip_atomic_store(a.host_rec + 4 * pd.slot, (int)a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

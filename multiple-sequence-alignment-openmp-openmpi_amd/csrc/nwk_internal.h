@@ -167,6 +167,12 @@ struct FillArgs {
   int* fin_pen;            // per slot (host-mapped)
   uint8_t* fin_hash;       // per slot, 64 raw bytes (host-mapped)
   unsigned* fin_flag;      // per slot (host-mapped): = epoch once the record is written
+  // Streamed host finalize (kCol, host-side finalize): the pair walk writes
+  // its moves to host-mapped ops_host + (ops_off - ops_base) and then, per
+  // slot, host_rec {flag = epoch, length (-1: left the window), end i, end j}
+  // (flag last, system scope), so host threads finalize pairs during the launch.
+  uint8_t* ops_host;
+  int* host_rec;
 };
 constexpr int kProfSyms = 6;  // kProfileDP: symbols + gap per column profile
 

@@ -186,6 +186,8 @@ struct nwk_ctx {
   // fused finalize (bits kernels): host-mapped coherent records the kernel
   // writes per pair as it is traced, {flag u32 [np] | penalty i32 [np] | hash [np][64]}
   HostBuf h_rec[2];
+  // streamed host finalize (kCol): host-mapped move strings and per-slot records {flag, length, end i, end j}
+  HostBuf h_opsm[2], h_hrec[2];
   // set while an nwk_align_pairs_begin call runs: align_work marks each
   // caller index whose final result is in place (nwk_align_pairs_poll)
   std::atomic<uint8_t>* ready_out = nullptr;
@@ -235,6 +237,7 @@ void nwk_ctx_destroy(nwk_ctx* c) {
   c->d_segctl.release(); c->d_colinfo.release(); c->d_prog.release(); c->d_pen.release(); c->d_hash.release(); c->d_hq.release();
   for (auto& b : c->d_msa) b.release();
   for (int b = 0; b < 2; ++b) { c->h_pen[b].release(); c->h_hash[b].release(); c->h_rec[b].release(); }
+  for (int b = 0; b < 2; ++b) { c->h_opsm[b].release(); c->h_hrec[b].release(); }
   c->h_tasks.release();
   for (int b = 0; b < 2; ++b) {
     c->h_pairs[b].release(); c->h_oplen[b].release(); c->h_endij[b].release(); c->h_ops[b].release();
@@ -642,9 +645,13 @@ void footprint(PairWork* w, int bits, int mode, bool affine) {
   if (mode == kCol) {
     const int64_t nb = ceil_div(w->m, kBitsRows), nw = ceil_div(w->n, 32);
     // segmented traceback (nwk_col.hip trace_col): a speculative segment per
-    // band but the last -- move buffers in segops, records and segment info in
-    // the control buffer.  NWK_COL_SEG=0: whole-pair walks only.
-    static const int seg_env = getenv("NWK_COL_SEG") ? atoi(getenv("NWK_COL_SEG")) : 1;
+    // band but the last -- move buffers in segops, records in d_segctl, info
+    // in d_colinfo.  Off unless NWK_COL_SEG=1: a segment started on a band's
+    // last row at the diagonal's column meets the pair's path only after
+    // ~500-5000 rows on random sequences (tools/probe/segconv.c), so the pair
+    // walk still crosses most of each band and then waits for the segment;
+    // measured C4 99.1 vs 91.3 ms per step, big13 26.3 vs 25.9 (r4n).
+    static const int seg_env = getenv("NWK_COL_SEG") ? atoi(getenv("NWK_COL_SEG")) : 0;
     const bool seg = seg_env != 0 && nb >= 2 && colseg_ok(w->n);
     w->spec = seg ? 1 : 0;
     w->nguess = 1;
@@ -1617,6 +1624,26 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       fa.fin_len = reinterpret_cast<int*>(fa.hq + np);
       fa.hq_ctl = c->d_ctl.as<unsigned>() + 32;  // (d_ctl's 256 bytes are zeroed per batch)
     }
+    // Streamed host finalize (nw_align_col batches finalized on the host: few
+    // long pairs, big13): the pair walk writes its moves into host-mapped
+    // memory and flags the pair, and host threads build rows and hashes while
+    // the launch still runs -- the pairs traced first (big13: 8 ms into a
+    // 24 ms launch) are done before it ends.  NWK_HOST_STREAM=0 disables.
+    static const int hstream_env = getenv("NWK_HOST_STREAM") ? atoi(getenv("NWK_HOST_STREAM")) : 1;
+    const bool hstream = pl.mode == kCol && !devhash && !fuse && a1 == nullptr && hstream_env != 0 && !fa.dbg_notrace;
+    fa.ops_host = nullptr;
+    fa.host_rec = nullptr;
+    if (hstream) {
+      if ((rc = c->h_opsm[par].ensure((size_t)ops + 256, hipHostMallocMapped | hipHostMallocCoherent)) != NWK_OK) return rc;
+      if ((rc = c->h_hrec[par].ensure(16 * (size_t)np, hipHostMallocMapped | hipHostMallocCoherent)) != NWK_OK) return rc;
+      memset(c->h_hrec[par].p, 0, 16 * (size_t)np);
+      void *dops = nullptr, *drec = nullptr;
+      HIP_TRY(hipHostGetDevicePointer(&dops, c->h_opsm[par].p, 0));
+      HIP_TRY(hipHostGetDevicePointer(&drec, c->h_hrec[par].p, 0));
+      fa.ops_host = static_cast<uint8_t*>(dops);
+      fa.host_rec = static_cast<int*>(drec);
+      fa.ops_base = ops_base_b;
+    }
     // One persistent launch: fill bands, and each pair's traceback runs on
     // the wave that finishes the pair's last band (nw_align).
     if (c->opts.verbose >= 3) {
@@ -1707,6 +1734,95 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         }
       });
     }
+    if (hstream) {
+      fin.join();
+      fsync = std::make_shared<FusedSync>();
+      const PairWork* dwf = dp.data() + pos;
+      const PairDesc* pdh = pd;  // (h_pairs[par] stays until batch b + 2)
+      const unsigned ep = fa.epoch;
+      const int* hrec = c->h_hrec[par].as<int>();
+      const uint8_t* hops = c->h_opsm[par].as<uint8_t>();
+      const int64_t obase = ops_base_b;
+      fin.start([c, np, dwf, pdh, fsync, ep, hrec, hops, obase, sc, penalties, hashes, chain]() {
+        // state per pair: 0 pending, 1 claimed, 2 finalized, 3 left the window (re-run)
+        std::unique_ptr<std::atomic<int>[]> state(new std::atomic<int>[(size_t)np]);
+        for (int64_t q = 0; q < np; ++q) state[q].store(0, std::memory_order_relaxed);
+        std::atomic<int64_t> nleft{np};
+        auto work = [&]() {
+          for (;;) {
+            const int d = fsync->done.load(std::memory_order_acquire);
+            if (d == 2 || nleft.load(std::memory_order_acquire) == 0) return;
+            bool any = false;
+            for (int64_t q = 0; q < np; ++q) {
+              if (state[q].load(std::memory_order_relaxed) != 0 || __atomic_load_n(hrec + 4 * q, __ATOMIC_ACQUIRE) != (int)ep)
+                continue;
+              int z = 0;
+              if (!state[q].compare_exchange_strong(z, 1)) continue;
+              any = true;
+              const int len = hrec[4 * q + 1];
+              if (len < 0) {
+                state[q].store(3, std::memory_order_release);
+              } else {
+                const PairWork& w = dwf[q];
+                Finalized f;
+                finalize_pair(c->seqs.data() + c->off[w.i], w.m, c->seqs.data() + c->off[w.j], w.n, sc,
+                              hops + (pdh[q].ops_off - obase), len, hrec[4 * q + 2], hrec[4 * q + 3], &f);
+                penalties[w.out] = f.penalty;
+                memcpy(hashes + 64 * w.out, f.hash, 64);
+                state[q].store(2, std::memory_order_release);
+              }
+              nleft.fetch_sub(1, std::memory_order_acq_rel);
+            }
+            if (!any) {
+              if (d == 1) return;  // the launch is over: every flag that will come has come
+              std::this_thread::sleep_for(std::chrono::microseconds(20));
+            }
+          }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < c->host_threads; ++t) pool.emplace_back(work);
+        // this thread: finalizes too, and reports finished pairs in slot order to the chain
+        std::vector<char> told((size_t)np, 0);
+        int64_t lo = 0;
+        auto report = [&]() {
+          bool any = false;
+          for (int64_t q = lo; q < np; ++q) {
+            if (told[(size_t)q] || state[q].load(std::memory_order_acquire) != 2) continue;
+            const PairWork& w = dwf[q];
+            if (chain) {
+              chain->prepare(w.out);
+              chain->ready[w.out] = 1;
+            }
+            mark_ready(c, w.out);
+            told[(size_t)q] = 1;
+            any = true;
+          }
+          while (lo < np && (told[(size_t)lo] || state[lo].load(std::memory_order_acquire) == 3)) ++lo;
+          if (chain && any) chain->advance();
+        };
+        std::thread rep_thread;
+        std::atomic<int> stop{0};
+        rep_thread = std::thread([&]() {
+          while (!stop.load(std::memory_order_acquire)) {
+            report();
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+          }
+          report();
+        });
+        work();
+        for (auto& t : pool) t.join();
+        stop.store(1, std::memory_order_release);
+        rep_thread.join();
+        if (fsync->done.load() == 2) return;
+        while (fsync->done.load(std::memory_order_acquire) == 0) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if (fsync->done.load() == 2) return;
+        for (int64_t q = 0; q < np; ++q) {
+          const int st_q = state[q].load();
+          const bool skipped = !fsync->skip.empty() && fsync->skip[(size_t)q];
+          if ((st_q != 2 && !skipped) || (st_q == 2 && skipped)) ++fsync->missing;
+        }
+      });
+    }
     if (c->opts.verbose >= 3) {
       fprintf(stderr, "nwk batch %d: launched mode %d bits %d grid %d, waiting\n", st.batches, pl.mode, pl.bits, grid);
       fflush(stderr);
@@ -1740,7 +1856,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       if ((rc = c->h_hash[par].ensure(64 * (size_t)np)) != NWK_OK) return rc;
       HIP_TRY(hipMemcpyAsync(c->h_pen[par].p, c->d_pen.p, 4 * (size_t)np, hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipMemcpyAsync(c->h_hash[par].p, c->d_hash.p, 64 * (size_t)np, hipMemcpyDeviceToHost, c->stream));
-    } else {
+    } else if (!hstream) {
       HIP_TRY(hipMemcpyAsync(c->h_ops[par].p, c->d_work.as<uint8_t>() + ops_base_b, (size_t)ops,
                              hipMemcpyDeviceToHost, c->stream));
     }
@@ -1878,7 +1994,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         st.window_retries += 1;
       }
     }
-    if (fuse) {  // the consumer finishes on its own; the next join collects it
+    if (fuse || hstream) {  // the consumer finishes on its own; the next join collects it
       fsync->skip = skip;
       fsync->done.store(1, std::memory_order_release);
       h_setup += tb1 - tb0;
