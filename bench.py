@@ -508,7 +508,7 @@ def main():
                  if st["mode"] == 7 else
                  "u32 bit planes (bit-sliced: 32 cells per VALU op, 2*pgap thermometer planes of the "
                  "G-space differences; int32-exact results, 2-bit traceback storage)"
-                 if st["mode"] in (8, 9) else ("int32" if st["bits"] == 32 else
+                 if st["mode"] in (8, 9, 10) else ("int32" if st["bits"] == 32 else
                                               "int32 (%d-bit mod-2^W traceback storage)" % st["bits"]),
         "data": "reference input file (mseq-big13-example.txt)" if args.workload == "big13"
                 else "synthetic (seeded MT19937 ACGT, workloads.py)",

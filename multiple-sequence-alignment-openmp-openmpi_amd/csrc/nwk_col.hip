@@ -934,7 +934,8 @@ __global__ __launch_bounds__(256) NWK_COL_OCC void nw_align_col(FillArgs a) {
     const int band = task.y;
     const int R0 = band * kBR;
     // the longest spans of a span-bound batch issue ahead of the other fill waves
-    if (pd.prio) __builtin_amdgcn_s_setprio(2);
+    if (pd.prio >= 2) __builtin_amdgcn_s_setprio(2);
+    else if (pd.prio == 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
     // code bit planes of rows R0 + 32 lane + b (rows past m: code 0, never traced)
     unsigned x0 = 0, x1 = 0;

@@ -502,9 +502,9 @@ int choose_plan(const nwk_ctx* c, const Scoring& sc, Plan* pl) {
   const bool want_bits = c->opts.kernel == 4 || c->opts.kernel == 5 || c->opts.kernel == 6 ||
                          (c->opts.kernel == 0 && bits_env != 0);
   if (want_bits && c->opts.bits == 0 && bits_admissible(pxy, pgap, c->alpha)) pl->mode = kBits;
-  // bit-parallel columns (nw_align_col, same domain): opts.kernel 6, or NWK_COL=1 under "auto"
-  static const int col_env = getenv("NWK_COL") ? atoi(getenv("NWK_COL")) : 0;
-  if (pl->mode == kBits && (c->opts.kernel == 6 || (c->opts.kernel == 0 && col_env == 1))) pl->mode = kCol;
+  // bit-parallel columns (nw_align_col, same domain): opts.kernel 6 (under
+  // "auto" use_col decides per job, once the pairs are known)
+  if (pl->mode == kBits && c->opts.kernel == 6) pl->mode = kCol;
   return NWK_OK;
 }
 
@@ -1104,6 +1104,29 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     const int want = c->opts.kernel == 5 ? 1 : c->opts.kernel == 4 ? 0 : strip_env;
     if (want != 0 && use_strips(c, work, sc.pgap, want == 1, &strip_ring)) pl.mode = kBitsStrip;
   }
+  // nw_align_col under "auto": a pair costs its span n + ~100 per band there
+  // against n + 2112 per band for nw_align_bits, and its stores are windowed
+  // (write-bound jobs), so it wins wherever the job is not many rounds of long
+  // bands: big13 24.1 vs 33 ms per step, C4 91 vs 100 ms, C3's 8-rank shard
+  // 34 vs 47 ms; C3 on one GPU (12 rounds of 50k-column bands) stays with
+  // nw_align_bits (153 vs 160 ms).  NWK_COL=0/1 forces (A/B runs).
+  if ((pl.mode == kBits || pl.mode == kBitsStrip) && c->opts.kernel == 0) {
+    static const int col_env = getenv("NWK_COL") ? atoi(getenv("NWK_COL")) : -1;
+    static const bool strip_forced = getenv("NWK_STRIP") && atoi(getenv("NWK_STRIP")) == 1;
+    bool col = col_env == 1;
+    if (col_env < 0 && !strip_forced) {
+      int64_t bands = 0;
+      int maxlen = 0;
+      for (const auto& w : work) {
+        if (w.m <= 0 || w.n <= 0) continue;
+        bands += ceil_div(w.m, kBitsRows);
+        maxlen = std::max(maxlen, std::max(w.m, w.n));
+      }
+      const double slots = 4.0 * col_blocks_per_cu(sc.pgap) * c->cus;
+      col = bands > 0 && (bands <= 3.0 * slots || maxlen <= 16384);
+    }
+    if (col) pl.mode = kCol;
+  }
   const bool bitsy = pl.mode == kBits || pl.mode == kBitsStrip || pl.mode == kCol;
   st.bits = bitsy ? 2 : pl.bits;
   st.mode = pl.mode;
@@ -1440,6 +1463,14 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       for (int q = 0; q < np; ++q) smax = std::max(smax, (double)pd[q].n + 100.0 * pd[q].nbands);
       for (int q = 0; q < np; ++q) pd[q].prio = (double)pd[q].n + 100.0 * pd[q].nbands >= 0.7 * smax ? 2 : 0;
     }
+    // kCol streamed batches (fused finalize: records leave during the launch;
+    // a sharded rank's pairs come in canonical piece order): the first 1/16 of
+    // the pairs dequeued -- a 16-piece rank's first piece -- fill at issue
+    // priority 2 and the next 1/16 at 1, so the first records are out early
+    // and rank 0's chain starts on them while the rest fills.  NWK_PIECE_PRIO=0 disables.
+    static const int piece_prio_env = getenv("NWK_PIECE_PRIO") ? atoi(getenv("NWK_PIECE_PRIO")) : 1;
+    if (pl.mode == kCol && piece_prio_env != 0 && devhash && c->opts.finalize == 3 && !sc.affine && np >= 32)
+      for (int q = 0; q < np; ++q) pd[q].prio = q < np / 16 ? 2 : q < np / 8 ? std::max(pd[q].prio, 1) : pd[q].prio;
     if ((rc = c->h_tasks.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
     int2* tk = c->h_tasks.as<int2>();
     // Pair-major (pairs already largest first): a pair's bands are dequeued
