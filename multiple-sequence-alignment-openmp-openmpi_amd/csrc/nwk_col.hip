@@ -368,10 +368,14 @@ __device__ __forceinline__ void walk_asm(unsigned WD, unsigned WU, unsigned WL, 
 // from a band's bottom to the merge.  A segment that fails (left the stored
 // window) is never merged into; a band whose segment never merges is walked
 // in full, as before.
-template <bool SPEC>
-__device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd, unsigned char* obuf, int lane, int sb,
-                                          int& o_len, int2& o_end, bool& o_out) {
-  const int nblk = pd.bits_nblk, win = pd.bits_w;
+// WIN: the pair has windowed storage (pd.bits_w > 0); without it the checked
+// walk is compiled out (its merge with the asm walk made the compiler
+// materialize an undefined phi input as a v_readfirstlane of the next tile's
+// load register, and so wait for that load on every pass)
+template <bool SPEC, bool WIN>
+__device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd, unsigned char* obuf, unsigned* pfl,
+                                          int lane, int sb, int& o_len, int2& o_end, bool& o_out) {
+  const int nblk = pd.bits_nblk, win = WIN ? pd.bits_w : 0;
   const int64_t bdw = (int64_t)nblk * 1024;  // dwords per band
   const unsigned* mat = a.mat + pd.mat_off;
   const bool segd = pd.spec_every > 0;
@@ -462,7 +466,7 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
   // the walk is predicted to leave the current one (rows per column ~ m / n),
   // through its left edge (64 columns on, 24 rows of slack above the entry
   // row) or its top (the row-lanes above, 16 columns of slack to the right).
-  unsigned vd[4] = {0, 0, 0, 0}, vu[4] = {0, 0, 0, 0}, nd[4] = {0, 0, 0, 0}, nu[4] = {0, 0, 0, 0};
+  unsigned vd[4] = {0, 0, 0, 0}, vu[4] = {0, 0, 0, 0};
   int cts = -1, tta = -1, ctb = -1, ncts = -1, nta = -1, nb_ = -1;
   // (pair walk) band bb's segment records of the tile's 128 rows, two per lane
   u64 rq[2] = {0, 0}, nrq[2] = {0, 0};
@@ -486,6 +490,29 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
       const unsigned* p = mat + (int64_t)bb * bdw + (int64_t)rel * 1024 + ((step & 7) >> 2) * 256 + 4 * t + (step & 3);
       d[k] = __builtin_nontemporal_load(p);
       u[k] = __builtin_nontemporal_load(p + 512);
+    }
+  };
+  // the tile ahead goes to LDS (pfl: 8 x 64 dwords per wave, d[k] at k * 64,
+  // u[k] at (4 + k) * 64) by LDS-DMA loads: no VGPR is the destination of a
+  // load in flight, so the compiler never waits on it inside the walk (with
+  // register destinations it did, for an undefined phi input it materialized
+  // from the first load's register)
+  const unsigned pfb = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)pfl);
+  auto prefetch_lds = [&](int bb, int blo_, int cts_, int ta_) {
+    const int cl = cts_ - lane;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int t = ta_ - k < 0 ? 0 : ta_ - k;
+      int step = cl + t;
+      int rel = (step >> 3) - blo_;
+      const bool okl = cl >= 0 && (unsigned)rel < (unsigned)nblk;
+      step = okl ? step : 0;
+      rel = okl ? rel : 0;
+      const unsigned* p = mat + (int64_t)bb * bdw + (int64_t)rel * 1024 + ((step & 7) >> 2) * 256 + 4 * t + (step & 3);
+      asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(p), "s"(__builtin_amdgcn_readfirstlane(pfb + 256u * k))
+                   : "memory", "m0");
+      asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(p + 512), "s"(__builtin_amdgcn_readfirstlane(pfb + 256u * (4 + k)))
+                   : "memory", "m0");
     }
   };
   auto rowlo_of = [](int ta_) { return ta_ > 3 ? 32 * (ta_ - 3) : 0; };
@@ -527,16 +554,16 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
       if (nb_ == b && c <= ncts && c > ncts - 64 && ta <= nta && r >= rowlo_of(nta)) {  // the tile ahead
 #if NWK_TRACE_PROF
         const u64 pw0 = __builtin_amdgcn_s_memtime();
-        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         p_wait += __builtin_amdgcn_s_memtime() - pw0;
 #endif
-        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the LDS-DMA loads)
         cts = ncts;
         tta = nta;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          vd[k] = nd[k];
-          vu[k] = nu[k];
+          vd[k] = pfl[64 * k + lane];
+          vu[k] = pfl[64 * (4 + k) + lane];
         }
         rq[0] = nrq[0];
         rq[1] = nrq[1];
@@ -575,7 +602,7 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
         }
       }
       if (nb_ >= 0) {
-        load_tile(b, blo, ncts, nta, nd, nu);
+        prefetch_lds(b, blo, ncts, nta);
         if (recs_on(b)) load_recs(b, nta, nrq);
       }
     }
@@ -651,7 +678,7 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
     // Tiles wholly inside skip the checks; near the window's edge each run's end
     // cells are checked (dev is linear along a D or U run)
     const int64_t ib = (int64_t)b * kBR;
-    const bool wchk = win > 0 && ((int64_t)cts * pd.m - (ib + trowlo) * pd.n > lim ||
+    const bool wchk = WIN && win > 0 && ((int64_t)cts * pd.m - (ib + trowlo) * pd.n > lim ||
                                   (int64_t)(cts - 63) * pd.m - (ib + trowlo + 127) * pd.n < -lim);
     auto outside = [&](int Ll, int Kk) {
       const int64_t dev = (int64_t)(cts - Ll) * pd.m - (ib + Kk - Ll) * pd.n;
@@ -779,13 +806,28 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
         }
       }
     };
-    if (wchk) {
-      walk(std::true_type{});
+    // (K and L pinned in SGPRs across the branch: an undefined phi input for
+    // them was materialized as v_readfirstlane of the next tile's load
+    // register, and the wait for that load then sat on every pass)
+    asm volatile("" : "+s"(K), "+s"(L));
+    // (the asm walk's operands: copies defined, and used, on both paths)
+    int Ka = K, La = L, mU = maxU;
+    u64 fL = finL;
+    if (WIN && wchk) {
+      asm volatile("" ::"s"(Ka), "s"(La), "s"(mU), "s"(fL));
+      if constexpr (WIN) walk(std::true_type{});
+      asm volatile("" : "+s"(K), "+s"(L));
     } else {
 #if NWK_COL_CWALK  // (A/B: the compiled walk)
       walk(std::false_type{});
 #else
-      walk_asm(WD, WU, WL, lane, Kb, trowlo, LL, K, L, finL, nUv, maxU);
+      unsigned nv = nUv;
+      walk_asm(WD, WU, WL, lane, Kb, trowlo, LL, Ka, La, fL, nv, mU);
+      K = Ka;
+      L = La;
+      finL = fL;
+      nUv = nv;
+      maxU = mU;
 #endif
     }
 #if NWK_TRACE_PROF
@@ -907,6 +949,7 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
 template <int NP, int SR, bool FUSE>
 __global__ __launch_bounds__(256) NWK_COL_OCC void nw_align_col(FillArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char obuf_all[4][kTraceRing];
+  __shared__ __attribute__((aligned(16))) unsigned pf_all[4][512];  // trace_col's tile ahead (LDS-DMA)
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   unsigned* prog = a.prog ? a.prog + blockIdx.x * 4 + wid : nullptr;  // NWK_WATCHDOG markers
@@ -1075,7 +1118,8 @@ __global__ __launch_bounds__(256) NWK_COL_OCC void nw_align_col(FillArgs a) {
 #if !defined(NWK_COL_TRACE_PRIO) || NWK_COL_TRACE_PRIO
       __builtin_amdgcn_s_setprio(3);
 #endif
-      trace_col<false>(a, pd, obuf_all[wid], lane, 0, tlen, tend, tout);
+      if (pd.bits_w > 0) trace_col<false, true>(a, pd, obuf_all[wid], pf_all[wid], lane, 0, tlen, tend, tout);
+      else trace_col<false, false>(a, pd, obuf_all[wid], pf_all[wid], lane, 0, tlen, tend, tout);
       __builtin_amdgcn_s_setprio(0);
       if constexpr (FUSE) {
         const bool ok_rows = !tout && fin_rows(a, pd, lane, tlen, tend);
@@ -1088,7 +1132,8 @@ __global__ __launch_bounds__(256) NWK_COL_OCC void nw_align_col(FillArgs a) {
       int2 tend;
       bool tout;
       __builtin_amdgcn_s_setprio(3);
-      trace_col<true>(a, pd, obuf_all[wid], lane, band, tlen, tend, tout);
+      if (pd.bits_w > 0) trace_col<true, true>(a, pd, obuf_all[wid], pf_all[wid], lane, band, tlen, tend, tout);
+      else trace_col<true, false>(a, pd, obuf_all[wid], pf_all[wid], lane, band, tlen, tend, tout);
       __builtin_amdgcn_s_setprio(0);
     }
   }
