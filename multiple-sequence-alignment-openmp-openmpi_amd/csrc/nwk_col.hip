@@ -129,10 +129,7 @@ __device__ __forceinline__ void col_hops(u64 (&c)[NP], unsigned (&acc)[NP], cons
 //   inj      the band above's last row for lane 0's columns of this half (bit q = column s_half + q)
 //   pub      CAP: acc after step s_half + 30's carries (columns s_half - 94 .. s_half - 63)
 //   MASK     steps of the first super-block: columns < 0 keep v = 0 (the left border)
-// TR: a transposed pair (PairDesc::tr): the up word stores ~[h > 0] of each
-// cell (h of row b = bit b + 1 of T_0, row 31's the carry out), so the walk's
-// U test reads "not LEFT" and its L runs "LEFT": DIAG > LEFT > UP
-template <int NP, int SR, bool MASK, bool CAP, int BLK, bool TR>
+template <int NP, int SR, bool MASK, bool CAP, int BLK>
 __device__ __forceinline__ void col_block(int s0, int lane, unsigned x0, unsigned x1, unsigned w0, unsigned w1,
                                           unsigned (&l)[NP], u64 (&c)[NP], unsigned (&acc)[NP],
                                           const u64 (&inj)[NP], unsigned (&pub)[NP], unsigned* st, bool sto) {
@@ -165,13 +162,7 @@ __device__ __forceinline__ void col_block(int s0, int lane, unsigned x0, unsigne
     if constexpr (SR < 0) dw[q] = match;
     else if constexpr (SR >= NP) dw[q] = ~0u;
     else dw[q] = BOP3(match, D[SR], D[SR], kA | ~kB);  // match | ~D_SR
-    if constexpr (TR) {
-      unsigned co;  // this lane's carry out of level 0: t_0 of its row 31
-      asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(co) : "s"(c[0]));
-      uw[q] = ~__builtin_amdgcn_alignbit(co, T[0], 1);  // ~[h > 0] of rows 0 .. 31
-    } else {
-      uw[q] = Vn[0];  // stored raw: UP is v == 0 (bit clear)
-    }
+    uw[q] = Vn[0];  // stored raw: UP is v == 0 (bit clear)
     if constexpr ((q & 3) == 3) {
       typedef unsigned u4 __attribute__((ext_vector_type(4)));
       constexpr int h = q >> 2;
@@ -399,8 +390,6 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
                  : a.ops_host ? a.ops_host + (pd.ops_off - a.ops_base)  // (streamed host finalize)
                               : a.ops + pd.ops_off;
   const unsigned ob = (unsigned)(uintptr_t)obuf;
-  // moves in the pair's own orientation: a transposed walk's U is the pair's L
-  const unsigned cU = pd.tr ? (unsigned)'L' : (unsigned)'U', cL = pd.tr ? (unsigned)'U' : (unsigned)'L';
   int Lc = 0, flushed = 0;
   auto flush = [&](int upto) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -858,10 +847,10 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
       const unsigned tot = (unsigned)__builtin_amdgcn_readlane((int)inc, 63);
       for (int j = 0; j < maxU; ++j)
         if ((unsigned)j < nU)
-          asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((Lc + (int)off + j) & (kTraceRing - 1))), "v"(cU)
+          asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((Lc + (int)off + j) & (kTraceRing - 1))), "v"((unsigned)'U')
                        : "memory");
       if (fin) {
-        const unsigned ch = ((finL >> lane) & 1ull) ? cL : (unsigned)'D';
+        const unsigned ch = ((finL >> lane) & 1ull) ? 'L' : 'D';
         asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((Lc + (int)(off + nU)) & (kTraceRing - 1))), "v"(ch)
                      : "memory");
       }
@@ -931,7 +920,6 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
 #endif
   o_len = out ? 0 : Lc;
   o_end = (a.dbg_notrace || out) ? make_int2(pd.m, pd.n) : make_int2(b * kBR + r + 1, c + 1);
-  if (pd.tr) o_end = make_int2(o_end.y, o_end.x);  // (the pair's own orientation)
   o_out = out;
   if (lane == 0) {
     a.oplen[pd.slot] = o_len;
@@ -1076,8 +1064,7 @@ __global__ __launch_bounds__(256) NWK_COL_OCC void nw_align_col(FillArgs a) {
         // lane's words of it hold a cell within bits_w columns of the diagonal
         const bool sto = (unsigned)rel < (unsigned)nblk && (!win || bits_lane_stored(hi0 + (int64_t)s0 * pd.m, lim, hlim));
         unsigned* st = mb + (int64_t)rel * 1024;
-        if (pd.tr) col_block<NP, SR, MASK, B == 3, B, true>(s0, lane, x0, x1, wc0, wc1, l, c, acc, inj, pub, st, sto);
-        else col_block<NP, SR, MASK, B == 3, B, false>(s0, lane, x0, x1, wc0, wc1, l, c, acc, inj, pub, st, sto);
+        col_block<NP, SR, MASK, B == 3, B>(s0, lane, x0, x1, wc0, wc1, l, c, acc, inj, pub, st, sto);
       };
       blk(std::integral_constant<int, 0>{});
       blk(std::integral_constant<int, 1>{});
@@ -1135,14 +1122,7 @@ __global__ __launch_bounds__(256) NWK_COL_OCC void nw_align_col(FillArgs a) {
       else trace_col<false, false>(a, pd, obuf_all[wid], pf_all[wid], lane, 0, tlen, tend, tout);
       __builtin_amdgcn_s_setprio(0);
       if constexpr (FUSE) {
-        PairDesc pf = pd;  // (fin_rows works in the pair's own orientation)
-        if (pd.tr) {
-          pf.x_off = pd.y_off;
-          pf.y_off = pd.x_off;
-          pf.m = pd.n;
-          pf.n = pd.m;
-        }
-        const bool ok_rows = !tout && fin_rows(a, pf, lane, tlen, tend);
+        const bool ok_rows = !tout && fin_rows(a, pd, lane, tlen, tend);
         hq_push(a, pd, lane, ok_rows);
       }
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();

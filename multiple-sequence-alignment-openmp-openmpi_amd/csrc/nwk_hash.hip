@@ -32,15 +32,7 @@ __global__ __launch_bounds__(256) void nw_rows(HashArgs h) {
   __shared__ int tx[4], ty[4];
   __shared__ long long sp[4];
   const int q = blockIdx.x;
-  PairDesc pd = h.pairs[q];
-  if (pd.tr) {  // nw_align_col ran the transposed matrix; moves and end are in the pair's orientation
-    const int64_t t = pd.x_off;
-    pd.x_off = pd.y_off;
-    pd.y_off = t;
-    const int u = pd.m;
-    pd.m = pd.n;
-    pd.n = u;
-  }
+  const PairDesc pd = h.pairs[q];
   const int nops = h.oplen[pd.slot];
   const int2 e = h.endij[pd.slot];
   const int pre = e.x > 0 ? e.x : e.y;

@@ -68,12 +68,6 @@ struct PairDesc {
   // column v % n' (0 = banded tasks)
   int32_t bits_np;
   int32_t prio;     // kCol: issue priority (s_setprio) of the pair's fill tasks -- the longest spans of a span-bound batch
-  // kCol: the fill and traceback run on the transposed matrix (x_off / y_off /
-  // e_off / m / n describe it: rows = the pair's y), storing "h > 0" where the
-  // UP bit would be (DIAG > LEFT > UP there is the reference's DIAG > UP > LEFT
-  // here); the walk emits moves and its end cell back in the pair's own
-  // orientation, and the finalize (fin_rows, nw_rows) swaps x and y back
-  int32_t tr;
   int64_t xw_off;   // kBitsStrip: y-window index of the row sequence's position 0 (its row codes)
 };
 

@@ -136,7 +136,6 @@ struct PairWork {
   int64_t njobs;                  // queued extra guesses (spec boundaries x (nguess - 1))
   int bits_w = 0;                 // kBits windowed storage: half-width in columns (0 = full), see PairDesc
   int bits_nblk = 0;              // kBits: stored 8-step blocks per band
-  int tr = 0;                     // kCol: fill the transposed matrix (PairDesc::tr); footprint in its dimensions
 };
 
 }  // namespace
@@ -644,8 +643,7 @@ void footprint(PairWork* w, int bits, int mode, bool affine) {
     return;
   }
   if (mode == kCol) {
-    const int fm = w->tr ? w->n : w->m, fn = w->tr ? w->m : w->n;  // the filled matrix's rows, columns
-    const int64_t nb = ceil_div(fm, kBitsRows), nw = ceil_div(fn, 32);
+    const int64_t nb = ceil_div(w->m, kBitsRows), nw = ceil_div(w->n, 32);
     // segmented traceback (nwk_col.hip trace_col): a speculative segment per
     // band but the last -- move buffers in segops, records in d_segctl, info
     // in d_colinfo.  Off unless NWK_COL_SEG=1: a segment started on a band's
@@ -654,13 +652,13 @@ void footprint(PairWork* w, int bits, int mode, bool affine) {
     // walk still crosses most of each band and then waits for the segment;
     // measured C4 99.1 vs 91.3 ms per step, big13 26.3 vs 25.9 (r4n).
     static const int seg_env = getenv("NWK_COL_SEG") ? atoi(getenv("NWK_COL_SEG")) : 0;
-    const bool seg = seg_env != 0 && nb >= 2 && colseg_ok(fn);
+    const bool seg = seg_env != 0 && nb >= 2 && colseg_ok(w->n);
     w->spec = seg ? 1 : 0;
     w->nguess = 1;
     w->njobs = 0;
-    w->segops_b = seg ? (nb - 1) * colseg_cap(fn) : 0;
+    w->segops_b = seg ? (nb - 1) * colseg_cap(w->n) : 0;
     w->segctl_b = seg ? (nb - 1) * ((int64_t)kBitsRows * 8 + 16) : 0;
-    w->bits_nblk = (int)col_nblk_of(fm, fn, w->bits_w);
+    w->bits_nblk = (int)col_nblk_of(w->m, w->n, w->bits_w);
     w->mat_dw = nb * w->bits_nblk * 1024;
     w->bnd_gr = (nb - 1) * nw * 4;  // NP <= 4 granules per 32 columns of each band's last row
     w->ops_b = round_up((int64_t)w->m + w->n, 128);  // (whole lines per pair: the fused finalize's rows)
@@ -1163,33 +1161,6 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       dp.push_back(w);
     }
   }
-  // nw_align_col: a pair costs its span, columns + ~100 per 2048-row band, so
-  // a pair much wider than tall (35k x 90k: 92k steps) is shorter transposed
-  // (90k x 35k: 39k steps) -- but with 2.4x the bands, which load every SIMD
-  // more.  So only a pair whose span is above the job's critical path (the
-  // longest of the pairs' shorter orientations) is transposed: big13 on one GPU
-  // is bound by its ~square 85k x 90k pairs and transposes nothing (all its wide
-  // pairs transposed: 24.9 -> 28.2 ms per step), while a rank of a sharded
-  // big13 whose longest pair is wide does (W = 8: 18.6 -> 17.1 ms).
-  // NWK_COL_TR=0 disables, 2 transposes every pair shorter so.
-  static const int tr_env = getenv("NWK_COL_TR") ? atoi(getenv("NWK_COL_TR")) : 1;
-  if (pl.mode == kCol && tr_env != 0 && !dp.empty()) {
-    auto spans = [](const PairWork& w) {
-      return std::make_pair((double)w.n + 100.0 * ceil_div(w.m, kBitsRows), (double)w.m + 100.0 * ceil_div(w.n, kBitsRows));
-    };
-    double crit = 0;
-    for (const auto& w : dp) {
-      const auto sp = spans(w);
-      crit = std::max(crit, std::min(sp.first, sp.second));
-    }
-    for (auto& w : dp) {
-      const auto sp = spans(w);
-      if (sp.second < 0.9 * sp.first && (tr_env == 2 || sp.first > 1.15 * crit)) {
-        w.tr = 1;
-        footprint(&w, pl.bits, pl.mode, sc.affine);
-      }
-    }
-  }
   if (!dp.empty()) {
     if ((rc = build_encoding(c, pl.kind)) != NWK_OK) return rc;
     if (bitsy && (rc = build_yw(c)) != NWK_OK) return rc;
@@ -1264,10 +1235,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     if (pl.mode == kCol && col_win_env < 0) {
       double cells = 0, bytes = 0, span = 0;
       for (const auto& w : dp) {
-        const int fm = w.tr ? w.n : w.m, fn = w.tr ? w.m : w.n;
         cells += (double)w.m * w.n;
         bytes += (double)w.m * w.n / 4;
-        span = std::max(span, (double)fn + 100.0 * (double)ceil_div(fm, kBitsRows));
+        span = std::max(span, (double)w.n + 100.0 * (double)ceil_div(w.m, kBitsRows));
       }
       col_wb = bytes / std::max(cells / 3.2e13, span * 3.0e-7) > 4e12;
     }
@@ -1449,23 +1419,19 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     for (int q = 0; q < np; ++q) {
       const PairWork& w = dp[pos + q];
       PairDesc& d = pd[q];
-      // (kCol transposed: rows = the pair's y, columns = its x)
-      const bool tr = pl.mode == kCol && w.tr;
-      const int ri = tr ? w.j : w.i, ci = tr ? w.i : w.j;
-      d.x_off = c->c_off[ri];
-      d.y_off = c->c_off[ci];
-      d.e_off = bitsy ? c->yw_off[ci] : c->e_off[ci];
+      d.x_off = c->c_off[w.i];
+      d.y_off = c->c_off[w.j];
+      d.e_off = bitsy ? c->yw_off[w.j] : c->e_off[w.j];
       d.xw_off = pl.mode == kBitsStrip ? c->yw_off[w.i] : 0;
       d.bits_np = pl.mode == kBitsStrip ? strip_np(w.n) : 0;
       d.prio = 0;
-      d.tr = tr ? 1 : 0;
       d.mat_off = mat_base_b / 4 + mo;
       d.bnd_off = bo;
       d.ops_off = ops_base_b + oo;
-      d.m = tr ? w.n : w.m;
-      d.n = tr ? w.m : w.n;
-      d.nbands = (int)ceil_div(d.m, bitsy ? kBitsRows : kBandRows);
-      d.nchunks = pl.mode == kBitsStrip ? d.bits_np / 64 : (int)ceil_div(d.n, 64);
+      d.m = w.m;
+      d.n = w.n;
+      d.nbands = (int)ceil_div(w.m, bitsy ? kBitsRows : kBandRows);
+      d.nchunks = pl.mode == kBitsStrip ? d.bits_np / 64 : (int)ceil_div(w.n, 64);
       d.sblocks = pl.mode == kBits        ? bits_sblocks(d.nchunks)
                   : pl.mode == kCol       ? col_sblocks(d.nchunks)
                   : pl.mode == kBitsStrip ? strip_sblocks(w.m, w.n)

@@ -160,33 +160,6 @@ def test_col_segmented_traceback_on_off(seg):
         assert o["hs"] == ohs
 
 
-@pytest.mark.parametrize("tr", ["0", "2"])
-def test_col_transposed_pairs(tr):
-    """Wide pairs filled on their transpose (PairDesc::tr: rows = the pair's y,
-    the stored UP word holding ~[h > 0] so DIAG > LEFT > UP there is the
-    reference's DIAG > UP > LEFT; moves and end cell swapped back), forced for
-    every pair whose transpose is shorter (NWK_COL_TR=2) and off (0), in a
-    child: 1-column and 1-row extremes, ragged bands, a short sequence inside a
-    long one (a long gap run), swapped halves; device and host finalize."""
-    r = random.Random(5150 + int(tr))
-    base = bytes(r.choice(ACGT) for _ in range(8000))
-    genes = [b"A", b"GT", base[:300], base[1000:3100], base, _mutants(r, base, 1, ACGT)[0],
-             bytes(r.choice(ACGT) for _ in range(4500))]
-    P, Q = (bytes(r.choice(ACGT) for _ in range(2500)) for _ in range(2))
-    genes += [P + Q, Q + P + P]
-    env = dict(os.environ, NWK_COL_TR=tr)
-    res = subprocess.run([sys.executable, "-c", _CHILD, os.path.dirname(seqalign.__file__), str(0)],
-                         input=json.dumps([g.hex() for g in genes]).encode(), env=env,
-                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
-    assert res.returncode == 0, res.stderr.decode()[-2000:]
-    out = json.loads(res.stdout.decode().strip().splitlines()[-1])
-    for (pxy, pgap), o in zip(((3, 2), (5, 1)), out):
-        assert o["mode"] == 10
-        _, opens, ohs = oracle.all_pairs(genes, pxy, pgap)
-        assert o["pen"] == opens
-        assert o["hs"] == ohs
-
-
 @pytest.mark.parametrize("win", ["auto", "48", "700", "3000"])
 def test_col_windowed_storage_and_full_rerun(win):
     """Windowed storage (NWK_BITS_WIN, read once per process: a child) with a
