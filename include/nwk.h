@@ -62,9 +62,11 @@ typedef struct nwk_opts {
                                 each pair's record reaches the host as soon as it is hashed (nwk_align_pairs_poll) */
   int32_t linear_space;      /* linear-space traceback: 0 = only for pairs whose matrix exceeds
                                 the HBM budget, -1 = never, G > 0 = every pair, G bands per recompute group */
-  int32_t kernel;            /* linear fill kernel: 0 auto (nw_align_bits where admissible: pxy >= 0, pgap 1 or 2,
-                                <= 4 symbols -- as 2048-row band tasks or, for jobs of many pairs per wave slot, as
-                                one rolling strip per pair, nw_align_strip), 1 nw_align, 2 nw_align_pk,
+  int32_t kernel;            /* linear fill kernel: 0 auto (where admissible -- pxy >= 0, pgap 1 or 2, <= 4
+                                symbols -- nw_align_col, unless the job is more than 3 rounds of wave slots of
+                                2048-row bands and has pairs longer than 16k, then nw_align_bits as band tasks or,
+                                for jobs of many pairs per wave slot, one rolling strip per pair, nw_align_strip;
+                                elsewhere the integer kernels), 1 nw_align, 2 nw_align_pk,
                                 3 nw_align_pk2, 4 nw_align_bits band tasks, 5 nw_align_strip wherever admissible
                                 (n / 64 in [63, 200] for pgap 2, [63, 500] for pgap 1), 6 nw_align_col (bit-parallel
                                 columns, nw_align_bits' domain; a kernel where it is not exact -- W > 4, mixed-sign K,
