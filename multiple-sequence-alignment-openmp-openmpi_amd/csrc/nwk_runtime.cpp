@@ -1475,7 +1475,12 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     // priority 2 and the next 1/16 at 1, so the first records are out early
     // and rank 0's chain starts on them while the rest fills.  NWK_PIECE_PRIO=0 disables.
     static const int piece_prio_env = getenv("NWK_PIECE_PRIO") ? atoi(getenv("NWK_PIECE_PRIO")) : 1;
-    if (pl.mode == kCol && piece_prio_env != 0 && devhash && c->opts.finalize == 3 && !sc.affine && np >= 32)
+    // (want_fuse: the fused finalize below, asked for or automatic)
+    static const int auto_fuse_env = getenv("NWK_AUTO_FUSE") ? atoi(getenv("NWK_AUTO_FUSE")) : 1;
+    const bool want_fuse = devhash && bitsy && !sc.affine &&
+                           (c->opts.finalize == 3 ||
+                            (c->opts.finalize == 0 && auto_fuse_env != 0 && chain && pl.mode == kCol && np >= 8192));
+    if (pl.mode == kCol && piece_prio_env != 0 && want_fuse && c->opts.finalize == 3 && np >= 32)
       for (int q = 0; q < np; ++q) pd[q].prio = q < np / 16 ? 2 : q < np / 8 ? std::max(pd[q].prio, 1) : pd[q].prio;
     if ((rc = c->h_tasks.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
     int2* tk = c->h_tasks.as<int2>();
@@ -1628,7 +1633,11 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     // host while it runs.  Only on request: on one GPU the separate nw_rows +
     // nw_hash is faster (C3 161.5 vs 165.4 ms per step, C4 100.9 vs 106.1),
     // but a rank of a sharded job can exchange and chain finished pairs early.
-    const bool fuse = devhash && c->opts.finalize == 3 && bitsy && !fa.dbg_notrace && !sc.affine;
+    // Automatic for nw_align_col getMinimumPenalties-style calls of >= 8,192
+    // pairs in a batch (C4: 32,640): with the separate finalize the chain's
+    // ~12.5 ms ran after the launch; with records streaming out of it the host
+    // chains while the launch runs.  NWK_AUTO_FUSE=0 disables.
+    const bool fuse = want_fuse && !fa.dbg_notrace;
     if (devhash) {
       if ((rc = c->d_pen.ensure(4 * (size_t)np)) != NWK_OK) return rc;
       if ((rc = c->d_hash.ensure(64 * (size_t)np)) != NWK_OK) return rc;
