@@ -1630,9 +1630,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     // finalize 3: the bits kernels' device finalize fused into the fill launch
     // (rows by the tracing wave, SHA-512 by waves that claim 32 traced pairs
     // from a queue: nwk_bits.hip fin_rows / hq_hash), records streaming to the
-    // host while it runs.  Only on request: on one GPU the separate nw_rows +
-    // nw_hash is faster (C3 161.5 vs 165.4 ms per step, C4 100.9 vs 106.1),
-    // but a rank of a sharded job can exchange and chain finished pairs early.
+    // host while it runs.  On request (a rank of a sharded job exchanges and
+    // chains finished pairs early); not for nw_align_bits on one GPU, where the
+    // separate nw_rows + nw_hash is faster (C3 161.5 vs 165.4 ms per step).
     // Automatic for nw_align_col getMinimumPenalties-style calls of >= 8,192
     // pairs in a batch (C4: 32,640): with the separate finalize the chain's
     // ~12.5 ms ran after the launch; with records streaming out of it the host
