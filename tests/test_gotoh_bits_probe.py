@@ -59,3 +59,27 @@ def test_gotoh_bits_score_longer_pairs(sim):
     inp = "3 3 1\n" + "".join("%s %s\n" % p for p in prs)
     out = subprocess.run([sim], input=inp, capture_output=True, text=True, check=True).stdout.split()
     assert [int(v) for v in out] == [oracle.score_affine(x, y, 3, 3, 1) for x, y in prs]
+
+
+@pytest.mark.gpu
+def test_gotoh_bits_gpu_band_scores():
+    """The step in nw_align_bits' anti-diagonal band layout on the GPU
+    (tools/probe/gotoh_gpu.hip, built by __graft_entry__.build): H[m][n] of
+    one-band pairs (m <= 2048) against the oracle, C5's scoring."""
+    exe = os.path.join(ROOT, "tools", "probe", "gotoh_gpu")
+    assert os.path.exists(exe), "tools/probe/gotoh_gpu not built (run __graft_entry__.build())"
+    rng = random.Random(23)
+    prs = []
+    for t in range(48):
+        m = [1, 2, 31, 32, 33, 2047, 2048][t] if t < 7 else rng.randint(1, 2048)
+        n = [1, 5, 64, 65, 3000, 1, 2100][t] if t < 7 else rng.randint(1, 3000)
+        x = "".join(rng.choice("ACGT") for _ in range(m))
+        if t % 4 == 1:
+            y = x[:n] + "".join(rng.choice("ACGT") for _ in range(max(0, n - m)))
+        else:
+            y = "".join(rng.choice("ACGT"[:rng.randint(2, 4)]) for _ in range(n))
+        prs.append((x, y))
+    inp = "".join("%s %s\n" % p for p in prs)
+    out = subprocess.run([exe, "check"], input=inp, capture_output=True, text=True, timeout=120, check=True)
+    got = [int(v) for v in out.stdout.split()]
+    assert got == [oracle.score_affine(x, y, 3, 3, 1) for x, y in prs]

@@ -44,49 +44,111 @@ struct Cfg {
   static_assert(SM <= VHI, "X's top must be VHI");
 };
 
+// Operand kinds, known at compile time: Z all zeros, O all ones, P a plane.
+enum { kZ = 0, kO = 1, kP = 2 };
+template <class C, int c>
+constexpr int kind_v() { return c <= C::VLO ? kO : (c > C::VHI ? kZ : kP); }
+template <class C, int q>
+constexpr int kind_q() { return q <= 0 ? kO : (q > C::NQ ? kZ : kP); }
+template <class C, int c>
+constexpr int kind_x() { return c <= C::XLO ? kO : (c > C::XHI ? kZ : kP); }
+
 // [x >= c] of a difference held as NV planes
 template <class C, int c>
 GB_HD uint32_t ge_v(const uint32_t (&P)[C::NV]) {
-  if constexpr (c <= C::VLO) return ~0u;
-  else if constexpr (c > C::VHI) return 0u;
+  if constexpr (kind_v<C, c>() == kO) return ~0u;
+  else if constexpr (kind_v<C, c>() == kZ) return 0u;
   else return P[c - C::VLO - 1];
 }
 // [x >= q] of a gap offset saturated at go
 template <class C, int q>
 GB_HD uint32_t ge_q(const uint32_t (&Q)[C::NQ > 0 ? C::NQ : 1]) {
-  if constexpr (q <= 0) return ~0u;
-  else if constexpr (q > C::NQ) return 0u;
+  if constexpr (kind_q<C, q>() == kO) return ~0u;
+  else if constexpr (kind_q<C, q>() == kZ) return 0u;
   else return Q[q - 1];
 }
 template <class C, int c>
 GB_HD uint32_t ge_x(const uint32_t (&X)[C::NX]) {
-  if constexpr (c <= C::XLO) return ~0u;
-  else if constexpr (c > C::XHI) return 0u;
+  if constexpr (kind_x<C, c>() == kO) return ~0u;
+  else if constexpr (kind_x<C, c>() == kZ) return 0u;
   else return X[c - C::XLO - 1];
 }
 
-// [Lv - min(e, go) >= c] = OR_{q=0..go} ([e <= q] & [Lv >= c + q])
-template <class C, int c, int q = 0>
-GB_HD uint32_t sub_gap(const uint32_t (&Lv)[C::NV], const uint32_t (&E)[C::NQ > 0 ? C::NQ : 1]) {
-  const uint32_t t = ~ge_q<C, q + 1>(E) & ge_v<C, c + q>(Lv);
-  if constexpr (q >= C::NQ) return t;
-  else return t | sub_gap<C, c, q + 1>(Lv, E);
+// acc | (a & b') with b' = NB ? ~b : b, one v_bitop3_b32 when both operands
+// are planes and acc holds earlier terms (HAS); constant operands fold away.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GB_OR_AND(acc, a, b) __builtin_amdgcn_bitop3_b32((acc), (a), (b), 0xF0u | (0xCCu & 0xAAu))
+#define GB_OR_ANDN(acc, a, b) __builtin_amdgcn_bitop3_b32((acc), (a), (b), 0xF0u | (0xCCu & ~0xAAu & 0xFFu))
+#define GB_OR_NOT(acc, b) __builtin_amdgcn_bitop3_b32((acc), (b), (b), 0xF0u | (~0xCCu & 0xFFu))
+#define GB_ANDN(a, b) __builtin_amdgcn_bitop3_b32((a), (b), (b), 0xF0u & ~0xCCu & 0xFFu)
+#else
+#define GB_OR_AND(acc, a, b) ((acc) | ((a) & (b)))
+#define GB_OR_ANDN(acc, a, b) ((acc) | ((a) & ~(b)))
+#define GB_OR_NOT(acc, b) ((acc) | ~(b))
+#define GB_ANDN(a, b) ((a) & ~(b))
+#endif
+template <int KA, int KB, bool NB>
+constexpr bool term_nonzero() {
+  constexpr int kb = NB ? (KB == kZ ? kO : (KB == kO ? kZ : kP)) : KB;
+  return KA != kZ && kb != kZ;
+}
+template <int KA, int KB, bool NB, bool HAS>
+GB_HD uint32_t acc_term(uint32_t acc, uint32_t a, uint32_t b) {
+  constexpr int kb = NB ? (KB == kZ ? kO : (KB == kO ? kZ : kP)) : KB;  // kind of b'
+  if constexpr (KA == kZ || kb == kZ) {
+    return acc;
+  } else if constexpr (KA == kO && kb == kO) {
+    return ~0u;
+  } else if constexpr (KA == kO) {  // the term is b'
+    const uint32_t t = NB ? ~b : b;
+    if constexpr (HAS) return NB ? GB_OR_NOT(acc, b) : (acc | b);
+    else return t;
+  } else if constexpr (kb == kO) {  // the term is a
+    if constexpr (HAS) return acc | a;
+    else return a;
+  } else {
+    if constexpr (HAS) return NB ? GB_OR_ANDN(acc, a, b) : GB_OR_AND(acc, a, b);
+    else return NB ? GB_ANDN(a, b) : (a & b);
+  }
 }
 
-// [X - Y >= c] = OR_{d = XLO..XHI} ([X >= d] & ~[Y >= d - c + 1])
-template <class C, int c, int d = C::XLO>
-GB_HD uint32_t diff_xv(const uint32_t (&X)[C::NX], const uint32_t (&Y)[C::NV]) {
-  const uint32_t t = ge_x<C, d>(X) & ~ge_v<C, d - c + 1>(Y);
-  if constexpr (d >= C::XHI) return t;
-  else return t | diff_xv<C, c, d + 1>(X, Y);
+// [Lv - min(e, go) >= c] = OR_{q=0..go} ([e <= q] & [Lv >= c + q]), accumulated
+// onto acc: term q is Lv_{c+q} & ~E_{q+1}.  Taken from q = go down: term go is
+// the plane Lv_{c+go} alone, which then starts the accumulator for free.
+template <class C, int c, bool HAS, int q = C::NQ>
+GB_HD uint32_t sub_gap(uint32_t acc, const uint32_t (&Lv)[C::NV], const uint32_t (&E)[C::NQ > 0 ? C::NQ : 1]) {
+  constexpr int KA = kind_v<C, c + q>(), KB = kind_q<C, q + 1>();
+  const uint32_t r = acc_term<KA, KB, true, HAS>(acc, ge_v<C, c + q>(Lv), ge_q<C, q + 1>(E));
+  constexpr bool has = HAS || term_nonzero<KA, KB, true>();
+  if constexpr (q <= 0) return r;
+  else return sub_gap<C, c, has, q - 1>(r, Lv, E);
+}
+template <class C, int c, int q = 0>
+constexpr bool sub_gap_any() {
+  if constexpr (q > C::NQ) return false;
+  else return term_nonzero<kind_v<C, c + q>(), kind_q<C, q + 1>(), true>() || sub_gap_any<C, c, q + 1>();
+}
+
+// [X - Y >= c] = OR_{d = XLO..XHI} ([X >= d] & ~[Y >= d - c + 1]).  Taken
+// from d = XHI down: term XLO is ~Y alone ([X >= XLO] holds), which then joins
+// the accumulator in the same instruction (acc | ~Y) instead of a v_not first.
+template <class C, int c, bool HAS = false, int d = C::XHI>
+GB_HD uint32_t diff_xv(uint32_t acc, const uint32_t (&X)[C::NX], const uint32_t (&Y)[C::NV]) {
+  constexpr int KA = kind_x<C, d>(), KB = kind_v<C, d - c + 1>();
+  const uint32_t r = acc_term<KA, KB, true, HAS>(acc, ge_x<C, d>(X), ge_v<C, d - c + 1>(Y));
+  constexpr bool has = HAS || term_nonzero<KA, KB, true>();
+  if constexpr (d <= C::XLO) return has ? r : 0u;
+  else return diff_xv<C, c, has, d - 1>(r, X, Y);
 }
 
 // [Y + min(e, go) >= q] = OR_{r=0..go} ([e >= r] & [Y >= q - r])
-template <class C, int q, int r = 0>
-GB_HD uint32_t add_gap(const uint32_t (&Y)[C::NV], const uint32_t (&E)[C::NQ > 0 ? C::NQ : 1]) {
-  const uint32_t t = ge_q<C, r>(E) & ge_v<C, q - r>(Y);
-  if constexpr (r >= C::NQ) return t;
-  else return t | add_gap<C, q, r + 1>(Y, E);
+template <class C, int q, bool HAS = false, int r = 0>
+GB_HD uint32_t add_gap(uint32_t acc, const uint32_t (&Y)[C::NV], const uint32_t (&E)[C::NQ > 0 ? C::NQ : 1]) {
+  constexpr int KA = kind_v<C, q - r>(), KB = kind_q<C, r>();
+  const uint32_t t = acc_term<KA, KB, false, HAS>(acc, ge_v<C, q - r>(Y), ge_q<C, r>(E));
+  constexpr bool has = HAS || term_nonzero<KA, KB, false>();
+  if constexpr (r >= C::NQ) return has ? t : 0u;
+  else return add_gap<C, q, has, r + 1>(t, Y, E);
 }
 
 template <class C, int p = 0>
@@ -94,15 +156,21 @@ GB_HD void x_planes(uint32_t match, const uint32_t (&L)[C::NV], const uint32_t (
                     const uint32_t (&U)[C::NV], const uint32_t (&fU)[C::NQ > 0 ? C::NQ : 1], uint32_t (&X)[C::NX]) {
   if constexpr (p < C::NX) {
     constexpr int c = C::XLO + 1 + p;
-    const uint32_t s = c <= C::SX ? ~0u : (c <= C::SM ? match : 0u);
-    X[p] = s | sub_gap<C, c>(L, eL) | sub_gap<C, c>(U, fU);
+    // [S >= c] first (ones, the match plane or nothing), then a's and b's terms
+    constexpr int KS = c <= C::SX ? kO : (c <= C::SM ? kP : kZ);
+    const uint32_t s0 = KS == kO ? ~0u : (KS == kP ? match : 0u);
+    constexpr bool hs = KS != kZ;
+    const uint32_t ra = sub_gap<C, c, hs>(s0, L, eL);
+    constexpr bool ha = hs || sub_gap_any<C, c>();
+    const uint32_t rb = sub_gap<C, c, ha>(ra, U, fU);
+    X[p] = (ha || sub_gap_any<C, c>()) ? rb : 0u;
     x_planes<C, p + 1>(match, L, eL, U, fU, X);
   }
 }
 template <class C, int p = 0>
 GB_HD void v_planes(const uint32_t (&X)[C::NX], const uint32_t (&Y)[C::NV], uint32_t (&out)[C::NV]) {
   if constexpr (p < C::NV) {
-    out[p] = diff_xv<C, C::VLO + 1 + p>(X, Y);
+    out[p] = diff_xv<C, C::VLO + 1 + p>(0u, X, Y);
     v_planes<C, p + 1>(X, Y, out);
   }
 }
@@ -110,7 +178,7 @@ template <class C, int q = 1>
 GB_HD void q_planes(const uint32_t (&Y)[C::NV], const uint32_t (&E)[C::NQ > 0 ? C::NQ : 1],
                     uint32_t (&out)[C::NQ > 0 ? C::NQ : 1]) {
   if constexpr (q <= C::NQ) {
-    out[q - 1] = add_gap<C, q>(Y, E);
+    out[q - 1] = add_gap<C, q>(0u, Y, E);
     q_planes<C, q + 1>(Y, E, out);
   }
 }
@@ -134,7 +202,7 @@ GB_HD void step(uint32_t match, const uint32_t (&L)[C::NV], const uint32_t (&eL)
   q_planes<C>(h, eL, e);
   q_planes<C>(v, fU, f);
   D = (match & ~ge_x<C, C::SM + 1>(X)) | (~match & ~ge_x<C, C::SX + 1>(X));
-  Fsrc = ~add_gap<C, 1>(v, fU);  // ~[f >= 1] (f's plane 0; go = 0 keeps no f planes)
+  Fsrc = ~add_gap<C, 1>(0u, v, fU);  // ~[f >= 1] (f's plane 0; go = 0 keeps no f planes)
   Eext = ~ge_q<C, C::NQ>(eL);
   Fext = ~ge_q<C, C::NQ>(fU);
   if constexpr (C::NQ == 0) {  // go = 0: every gap cell may open (ties open)
