@@ -11,7 +11,7 @@
 //   gotoh_gpu check < pairs      rows of stdin "x y" (|x| <= 2048): prints H[m][n]
 //                                per pair (tests/test_gotoh_bits_probe.py checks
 //                                it against the oracle)
-//   gotoh_gpu rate [waves] [n] [store]
+//   gotoh_gpu rate [waves] [n] [store] [occ]
 //                                random pairs, 2048 x n cells per wave, prints
 //                                GCUPS; store = 1 writes the four traceback words
 //                                of every step (0.5 B per cell, no window)
@@ -53,8 +53,8 @@ struct Task {
   int m, n;
 };
 
-template <bool CHECK, bool STORE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void gotoh_band(
+template <bool CHECK, bool STORE, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void gotoh_band(
     const Task* tasks, int ntasks, long long* out, unsigned* sink, unsigned* st) {
   const int lane = threadIdx.x & 63;
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -204,7 +204,7 @@ static void add_pair(Host& H, const std::string& x, const std::string& y) {
   H.tasks.push_back(Task{nullptr, nullptr, m, n});
 }
 
-template <bool CHECK, bool STORE>
+template <bool CHECK, bool STORE, int OCC = 4>
 static double run(Host& H, std::vector<long long>& res, int reps) {
   unsigned *dx, *dy, *dsink, *dst = nullptr;
   Task* dt;
@@ -228,11 +228,11 @@ static double run(Host& H, std::vector<long long>& res, int reps) {
   hipEvent_t a, b;
   HIPCHK(hipEventCreate(&a));
   HIPCHK(hipEventCreate(&b));
-  hipLaunchKernelGGL((gotoh_band<CHECK, STORE>), dim3(grid), dim3(256), 0, 0, dt, nt, dout, dsink, dst);  // warm-up
+  hipLaunchKernelGGL((gotoh_band<CHECK, STORE, OCC>), dim3(grid), dim3(256), 0, 0, dt, nt, dout, dsink, dst);  // warm-up
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipEventRecord(a));
   for (int r = 0; r < reps; ++r)
-    hipLaunchKernelGGL((gotoh_band<CHECK, STORE>), dim3(grid), dim3(256), 0, 0, dt, nt, dout, dsink, dst);
+    hipLaunchKernelGGL((gotoh_band<CHECK, STORE, OCC>), dim3(grid), dim3(256), 0, 0, dt, nt, dout, dsink, dst);
   HIPCHK(hipEventRecord(b));
   HIPCHK(hipEventSynchronize(b));
   HIPCHK(hipGetLastError());
@@ -262,16 +262,18 @@ int main(int argc, char** argv) {
   const int waves = argc > 2 ? std::atoi(argv[2]) : 8192;
   const int n = argc > 3 ? std::atoi(argv[3]) : 4096;
   const bool store = argc > 4 && std::atoi(argv[4]) != 0;
+  const int occ = argc > 5 ? std::atoi(argv[5]) : 4;  // waves per SIMD the register budget is cut for (4 or 5)
   if (waves < 1 || waves > 65536 || n < 32 || n > 1 << 20) { std::fprintf(stderr, "bad size\n"); return 2; }
   srand(1);
   std::string x(2048, 'A'), y(n, 'A');
   for (auto& c : x) c = "ACGT"[rand() & 3];
   for (auto& c : y) c = "ACGT"[rand() & 3];
   for (int w = 0; w < waves; ++w) add_pair(H, x, y);  // one pair's data, many waves (rate only)
-  const double ms = store ? run<false, true>(H, res, 3) : run<false, false>(H, res, 3);
+  const double ms = occ == 5 ? (store ? run<false, true, 5>(H, res, 3) : run<false, false, 5>(H, res, 3))
+                             : (store ? run<false, true, 4>(H, res, 3) : run<false, false, 4>(H, res, 3));
   const double cells = (double)waves * 2048.0 * n;
   const double steps = (double)n + 2048 + 32;
-  std::printf("{\"waves\": %d, \"n\": %d, \"store\": %d, \"ms\": %.3f, \"gcups\": %.1f, \"ns_per_wave_step\": %.2f}\n",
-              waves, n, (int)store, ms, cells / ms / 1e6, ms * 1e6 / steps);
+  std::printf("{\"waves\": %d, \"n\": %d, \"store\": %d, \"occ\": %d, \"ms\": %.3f, \"gcups\": %.1f, \"ns_per_wave_step\": %.2f}\n",
+              waves, n, (int)store, occ, ms, cells / ms / 1e6, ms * 1e6 / steps);
   return 0;
 }
