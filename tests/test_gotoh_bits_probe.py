@@ -83,3 +83,27 @@ def test_gotoh_bits_gpu_band_scores():
     out = subprocess.run([exe, "check"], input=inp, capture_output=True, text=True, timeout=120, check=True)
     got = [int(v) for v in out.stdout.split()]
     assert got == [oracle.score_affine(x, y, 3, 3, 1) for x, y in prs]
+
+
+@pytest.mark.gpu
+def test_gotoh_bits_gpu_chained_bands():
+    """The same step with band hand-off (tools/probe/gotoh_chain.hip: each band's
+    last row published as {epoch | plane word} granules and polled by the band
+    below): pairs of 1-4 bands against the oracle's H[m][n], C5's scoring."""
+    exe = os.path.join(ROOT, "tools", "probe", "gotoh_chain")
+    assert os.path.exists(exe), "tools/probe/gotoh_chain not built (run __graft_entry__.build())"
+    rng = random.Random(29)
+    prs = []
+    sizes = [(2048, 100), (2049, 100), (4096, 64), (4097, 1), (1, 5000), (6000, 33), (5000, 2500), (7000, 3000)]
+    for t in range(24):
+        m, n = sizes[t] if t < len(sizes) else (rng.randint(1, 7000), rng.randint(1, 3000))
+        x = "".join(rng.choice("ACGT") for _ in range(m))
+        if t % 3 == 1:
+            y = x[:n] + "".join(rng.choice("ACGT") for _ in range(max(0, n - m)))
+        else:
+            y = "".join(rng.choice("ACGT"[:rng.randint(2, 4)]) for _ in range(n))
+        prs.append((x, y))
+    inp = "".join("%s %s\n" % p for p in prs)
+    out = subprocess.run([exe, "check"], input=inp, capture_output=True, text=True, timeout=120, check=True)
+    got = [int(v) for v in out.stdout.split()]
+    assert got == [oracle.score_affine(x, y, 3, 3, 1) for x, y in prs]

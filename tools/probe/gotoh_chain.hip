@@ -1,0 +1,369 @@
+// gotoh_chain.hip -- the bit-sliced Gotoh step (gotoh_bits.h) with band
+// hand-off: pairs of any height, 2048-row bands in a chain, one wave per band.
+//
+// Layout as gotoh_gpu.hip (bit b of lane t = row R0 + 32 t + b + 1, at column
+// s - 32 t - b at step s).  A band's last row (lane 63, bit 31: column
+// s - 2047) goes to an LDS ring each step; at the end of every 32-step segment
+// the next complete 32 columns are packed by ballot into 11 plane words (8 of
+// h, 3 of f) and published as self-tagged granules {epoch:32 | word:32}.  The
+// band below polls them with atomic reads (the coherence point, as
+// nw_align_bits' bits_wait) and stages one word per plane into LDS, bit 31 per
+// column, as the DPP fill-in of lane 0.  Tasks are dequeued from one counter
+// in dependency order (band-major), so a band's producer is always running.
+//
+//   gotoh_chain check < pairs    "x y" per line, any |x|: H[m][n] per pair
+//   gotoh_chain rate [pairs] [m] [n]
+//                                pairs random m x n pairs, prints GCUPS (fill only,
+//                                no traceback stores)
+//
+// C5's scoring (pxy 3, go 3, ge 1).  A probe: not part of libnwk.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "gotoh_bits.h"
+
+using namespace gotoh_bits;
+using C5 = Cfg<3, 1, 3>;
+constexpr int kGO = 3;
+constexpr int NQ1 = C5::NQ > 0 ? C5::NQ : 1;
+constexpr int kPl = C5::NV + NQ1;  // planes handed down: h then f (11)
+constexpr int kPs = 12;            // LDS / granule stride per column / chunk
+
+typedef unsigned long long u64;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+#define RLX __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
+#define HIPCHK(x)                                                                  \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      std::exit(1);                                                                \
+    }                                                                              \
+  } while (0)
+
+struct Pair {
+  const unsigned* xp;  // [nb * 64][2] row code planes
+  const unsigned* yr;  // [(n >> 5) + 4][2] reversed column chunks (gotoh_gpu.hip)
+  u64* hand;           // [nb][nw][kPs] granules of each band's last row
+  long long* out;      // sum of v over column n, all rows (atomic)
+  int m, n, nb, nw;    // nw = (n >> 5) + 1 chunks of 32 columns
+};
+
+__device__ __forceinline__ u64 opaque_zero() {
+  u64 z = 0;
+  asm volatile("" : "+v"(z));
+  return z;
+}
+
+template <bool CHECK>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void gotoh_chain(
+    const Pair* pairs, const int2* tasks, int ntasks, unsigned* counter, unsigned* err, unsigned epoch,
+    unsigned* sink) {
+  __shared__ __attribute__((aligned(16))) unsigned cons_all[4][32 * kPs];
+  __shared__ __attribute__((aligned(16))) unsigned ring_all[4][64 * kPs];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  unsigned* cons = cons_all[wid];
+  unsigned* ring = ring_all[wid];
+  unsigned sk = 0;
+  for (;;) {
+    unsigned tk = 0;
+    if (lane == 0) tk = atomicAdd(counter, 1u);
+    tk = __builtin_amdgcn_readfirstlane(tk);
+    if (tk >= (unsigned)ntasks) break;
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)err, RLX)) != 0u) break;
+    const int2 task = tasks[tk];
+    const Pair P = pairs[task.x];
+    const int band = task.y;
+    const int R0 = band * 2048;
+    const unsigned x0 = P.xp[2 * (band * 64 + lane)], x1 = P.xp[2 * (band * 64 + lane) + 1];
+    const u64* gin = P.hand + ((size_t)(band > 0 ? band - 1 : 0) * P.nw) * kPs;
+    u64* gout = P.hand + ((size_t)band * P.nw) * kPs;
+    const bool to_below = band + 1 < P.nb;
+    const int kmax = P.n >> 5;  // last chunk holding a real column
+    uint32_t v[C5::NV], e[NQ1], h[C5::NV], f[NQ1];
+    const uint32_t row1 = (band == 0 && lane == 0) ? 1u : 0u;  // v(1, 0) = -go
+#pragma unroll
+    for (int p = 0; p < C5::NV; ++p) {
+      v[p] = p < kGO ? ~row1 : 0u;
+      h[p] = 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ1; ++q) e[q] = f[q] = ~0u;
+    const int nsteps = P.n + 2048 + 32;
+    long long acc = 0;
+    bool ok = true;
+    for (int s0 = 0; s0 < nsteps && ok; s0 += 32) {
+      const int j = s0 >> 5;
+      // --- the row above for lane 0's columns 32 j .. 32 j + 31 -> cons (bit 31)
+      {
+        unsigned w = 0;  // lane p < kPl: plane p's word (bit r = column 32 j + r)
+        if (band == 0) {  // row 0: h(0, 1) = -go (no plane), h(0, c > 1) = 0 (planes < go), f = +inf
+          const unsigned h0 = j == 0 ? ~3u : ~0u;  // columns 0 and 1 cleared in chunk 0
+          w = lane < kGO ? h0 : (lane < C5::NV ? 0u : ~0u);
+        } else if (j <= kmax) {
+          u64 g = lane < kPl ? __hip_atomic_fetch_add((gu64*)(gin + (size_t)j * kPs + lane), opaque_zero(), RLX) : 0;
+          const u64 t0 = __builtin_amdgcn_s_memrealtime();
+          while (!__all(lane >= kPl || (unsigned)(g >> 32) == epoch)) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull ||
+                __builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)err, RLX)) != 0u) {
+              if (lane == 0) atomicOr(err, 1u);
+              ok = false;
+              break;
+            }
+            if (lane < kPl) g = __hip_atomic_fetch_add((gu64*)(gin + (size_t)j * kPs + lane), opaque_zero(), RLX);
+          }
+          w = (unsigned)g;
+        }
+        // lane r < 32 writes column 32 j + r's entry: plane p's bit at bit 31
+#pragma unroll
+        for (int p = 0; p < kPl; ++p) {
+          const unsigned wp = (unsigned)__builtin_amdgcn_readlane((int)w, p);
+          if (lane < 32) cons[lane * kPs + p] = ((wp >> lane) & 1u) << 31;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      const int q = j - lane;
+      const int qi = q < -1 ? -1 : (q > kmax + 1 ? kmax + 1 : q);
+      const unsigned lo0 = P.yr[2 * (qi + 2)], lo1 = P.yr[2 * (qi + 2) + 1];
+      const unsigned hi0 = P.yr[2 * (qi + 1)], hi1 = P.yr[2 * (qi + 1) + 1];
+      auto seg = [&](auto mask_t) {
+        constexpr bool mask = decltype(mask_t)::value;
+#pragma unroll 4
+        for (int r = 0; r < 32; ++r) {
+          const int s = s0 + r;
+          const unsigned sh = 31u - (unsigned)r;
+          const unsigned y0 = __builtin_amdgcn_alignbit(hi0, lo0, sh);
+          const unsigned y1 = __builtin_amdgcn_alignbit(hi1, lo1, sh);
+          const uint32_t match = ~((x0 ^ y0) | (x1 ^ y1));
+          const uint4 ca = *reinterpret_cast<const uint4*>(cons + r * kPs);
+          const uint4 cb = *reinterpret_cast<const uint4*>(cons + r * kPs + 4);
+          const uint4 cc = *reinterpret_cast<const uint4*>(cons + r * kPs + 8);
+          const unsigned inj[12] = {ca.x, ca.y, ca.z, ca.w, cb.x, cb.y, cb.z, cb.w, cc.x, cc.y, cc.z, cc.w};
+          uint32_t U[C5::NV], fU[NQ1];
+#pragma unroll
+          for (int p = 0; p < C5::NV; ++p) {
+            const unsigned T = (unsigned)__builtin_amdgcn_update_dpp((int)inj[p], (int)h[p], 0x138, 0xf, 0xf, false);
+            U[p] = __builtin_amdgcn_alignbit(h[p], T, 31);
+          }
+#pragma unroll
+          for (int p = 0; p < NQ1; ++p) {
+            const unsigned T =
+                (unsigned)__builtin_amdgcn_update_dpp((int)inj[C5::NV + p], (int)f[p], 0x138, 0xf, 0xf, false);
+            fU[p] = __builtin_amdgcn_alignbit(f[p], T, 31);
+          }
+          uint32_t D, Fs, Ee, Fe, vn[C5::NV], en[NQ1];
+          step<C5>(match, v, e, U, fU, vn, en, h, f, D, Fs, Ee, Fe);
+#pragma unroll
+          for (int p = 0; p < C5::NV; ++p) v[p] = vn[p];
+#pragma unroll
+          for (int qq = 0; qq < NQ1; ++qq) e[qq] = en[qq];
+          if constexpr (mask) {  // columns <= 0 keep the left border
+            const int lim = s - 32 * lane;
+            const uint32_t M = lim <= 0 ? ~0u : (lim >= 32 ? 0u : ~((1u << lim) - 1u));
+#pragma unroll
+            for (int p = 0; p < C5::NV; ++p) v[p] = (v[p] & ~M) | ((p < kGO ? ~row1 : 0u) & M);
+#pragma unroll
+            for (int qq = 0; qq < NQ1; ++qq) e[qq] |= M;
+          }
+          if (to_below && lane == 63) {  // the band's last row at column s - 2047
+            unsigned* en_ = ring + ((s - 2047) & 63) * kPs;
+            *reinterpret_cast<uint4*>(en_) = make_uint4(h[0], h[1], h[2], h[3]);
+            *reinterpret_cast<uint4*>(en_ + 4) = make_uint4(h[4], h[5], h[6], h[7]);
+            *reinterpret_cast<uint4*>(en_ + 8) = make_uint4(f[0], f[1], f[2], 0u);
+          }
+          if constexpr (CHECK) {
+            const int b = s - P.n - 32 * lane;
+            if (b >= 0 && b < 32 && R0 + 32 * lane + b < P.m) {
+              int vv = C5::VLO;
+#pragma unroll
+              for (int p = 0; p < C5::NV; ++p) vv += (int)((v[p] >> b) & 1u);
+              acc += vv;
+            }
+          }
+          sk ^= D;
+        }
+      };
+      if (s0 < 2048 + 32) seg(std::true_type{});
+      else seg(std::false_type{});
+      // --- publish chunk k = j - 64 (columns 32 k .. + 31, complete after this segment)
+      const int k = j - 64;
+      if (to_below && k >= 0 && k <= kmax) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        unsigned word = 0;
+#pragma unroll
+        for (int p = 0; p < kPl; ++p) {
+          const unsigned bit = lane < 32 ? ring[((32 * k + lane) & 63) * kPs + p] >> 31 : 0u;
+          const unsigned wd = (unsigned)__ballot(bit != 0u);
+          word = lane == p ? wd : word;
+        }
+        if (lane < kPl) __hip_atomic_store((gu64*)(gout + (size_t)k * kPs + lane), ((u64)epoch << 32) | word, RLX);
+      }
+    }
+    if (CHECK && ok) {
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+      if (lane == 0) atomicAdd((unsigned long long*)P.out, (unsigned long long)acc);
+    }
+  }
+  sink[(blockIdx.x * 4 + wid) * 64 + lane] = sk;
+}
+
+static int code(char c) { return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : 3; }
+
+struct HostPair {
+  std::vector<unsigned> xp, yr;
+  int m, n, nb;
+};
+
+static HostPair build_pair(const std::string& x, const std::string& y) {
+  HostPair H;
+  H.m = (int)x.size();
+  H.n = (int)y.size();
+  H.nb = (H.m + 2047) / 2048;
+  for (int t = 0; t < 64 * H.nb; ++t) {
+    unsigned p0 = 0, p1 = 0;
+    for (int b = 0; b < 32; ++b) {
+      const int i = 32 * t + b;
+      const int c = i < H.m ? code(x[i]) : 0;
+      p0 |= (unsigned)(c & 1) << b;
+      p1 |= (unsigned)(c >> 1) << b;
+    }
+    H.xp.push_back(p0);
+    H.xp.push_back(p1);
+  }
+  const int nq = (H.n >> 5) + 1;
+  for (int q = -2; q <= nq; ++q) {
+    unsigned w0 = 0, w1 = 0;
+    for (int r = 0; r < 32; ++r) {
+      const int col = 32 * q + r;
+      const int c = (col >= 1 && col <= H.n) ? code(y[col - 1]) : 0;
+      w0 |= (unsigned)(c & 1) << (31 - r);
+      w1 |= (unsigned)(c >> 1) << (31 - r);
+    }
+    H.yr.push_back(w0);
+    H.yr.push_back(w1);
+  }
+  return H;
+}
+
+// uploads `hp` (shared device copies for identical pairs when `same`), runs
+// `reps` timed launches after one warm-up; returns ms per launch
+static double run(const std::vector<HostPair>& hp, bool check, int reps, std::vector<long long>& out, bool same) {
+  const int np = (int)hp.size();
+  std::vector<Pair> P(np);
+  std::vector<void*> allocs;
+  int maxb = 0;
+  for (int i = 0; i < np; ++i) {
+    const HostPair& H = hp[i];
+    unsigned *dx, *dy;
+    if (!same || i == 0) {
+      HIPCHK(hipMalloc(&dx, H.xp.size() * 4));
+      HIPCHK(hipMalloc(&dy, H.yr.size() * 4));
+      HIPCHK(hipMemcpy(dx, H.xp.data(), H.xp.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(dy, H.yr.data(), H.yr.size() * 4, hipMemcpyHostToDevice));
+      allocs.push_back(dx);
+      allocs.push_back(dy);
+    } else {
+      dx = const_cast<unsigned*>(P[0].xp);
+      dy = const_cast<unsigned*>(P[0].yr);
+    }
+    const int nw = (H.n >> 5) + 1;
+    u64* hand;
+    HIPCHK(hipMalloc(&hand, (size_t)H.nb * nw * kPs * 8));
+    HIPCHK(hipMemset(hand, 0, (size_t)H.nb * nw * kPs * 8));
+    allocs.push_back(hand);
+    P[i] = Pair{dx, dy, hand, nullptr, H.m, H.n, H.nb, nw};
+    maxb = std::max(maxb, H.nb);
+  }
+  long long* dout;
+  HIPCHK(hipMalloc(&dout, 8 * np));
+  for (int i = 0; i < np; ++i) P[i].out = dout + i;
+  std::vector<int2> tk;  // band-major: every band's producer is dequeued before it
+  for (int b = 0; b < maxb; ++b)
+    for (int i = 0; i < np; ++i)
+      if (b < hp[i].nb) tk.push_back(make_int2(i, b));
+  Pair* dp;
+  int2* dt;
+  unsigned *dctr, *derr, *dsink;
+  HIPCHK(hipMalloc(&dp, sizeof(Pair) * np));
+  HIPCHK(hipMemcpy(dp, P.data(), sizeof(Pair) * np, hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&dt, sizeof(int2) * tk.size()));
+  HIPCHK(hipMemcpy(dt, tk.data(), sizeof(int2) * tk.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&dctr, 4));
+  HIPCHK(hipMalloc(&derr, 4));
+  HIPCHK(hipMemset(derr, 0, 4));
+  int dev = 0, cus = 0;
+  HIPCHK(hipGetDevice(&dev));
+  HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int grid = cus * 4;  // 4 waves per SIMD, persistent
+  HIPCHK(hipMalloc(&dsink, (size_t)grid * 256 * 4));
+  hipEvent_t a, b;
+  HIPCHK(hipEventCreate(&a));
+  HIPCHK(hipEventCreate(&b));
+  double ms_sum = 0;
+  for (int r = 0; r <= reps; ++r) {  // launch 0 is the warm-up; every launch has a fresh epoch
+    HIPCHK(hipMemset(dctr, 0, 4));
+    HIPCHK(hipMemset(dout, 0, 8 * np));
+    HIPCHK(hipEventRecord(a));
+    if (check) hipLaunchKernelGGL(gotoh_chain<true>, dim3(grid), dim3(256), 0, 0, dp, dt, (int)tk.size(), dctr, derr, 1u + r, dsink);
+    else hipLaunchKernelGGL(gotoh_chain<false>, dim3(grid), dim3(256), 0, 0, dp, dt, (int)tk.size(), dctr, derr, 1u + r, dsink);
+    HIPCHK(hipEventRecord(b));
+    HIPCHK(hipEventSynchronize(b));
+    HIPCHK(hipGetLastError());
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, a, b));
+    if (r > 0) ms_sum += ms;
+  }
+  unsigned herr = 0;
+  HIPCHK(hipMemcpy(&herr, derr, 4, hipMemcpyDeviceToHost));
+  if (herr) { std::fprintf(stderr, "gotoh_chain: wait timed out (err %u)\n", herr); std::exit(4); }
+  out.resize(np);
+  HIPCHK(hipMemcpy(out.data(), dout, 8 * np, hipMemcpyDeviceToHost));
+  for (void* p : allocs) (void)hipFree(p);
+  (void)hipFree(dout); (void)hipFree(dp); (void)hipFree(dt); (void)hipFree(dctr); (void)hipFree(derr); (void)hipFree(dsink);
+  return reps > 0 ? ms_sum / reps : 0.0;
+}
+
+int main(int argc, char** argv) {
+  const std::string mode = argc > 1 ? argv[1] : "rate";
+  std::vector<HostPair> hp;
+  std::vector<long long> sums;
+  if (mode == "check") {
+    std::vector<std::pair<int, int>> mn;
+    std::string x, y;
+    while (std::cin >> x >> y) {
+      if (x.empty() || y.empty() || x.size() > (1u << 20) || y.size() > (1u << 20)) { std::fprintf(stderr, "bad pair\n"); return 2; }
+      hp.push_back(build_pair(x, y));
+    }
+    run(hp, true, 0, sums, false);
+    for (size_t i = 0; i < hp.size(); ++i)  // H = G(0, n) - sum v + (m + n) ge
+      std::printf("%lld\n", kGO - sums[i] + (long long)(hp[i].m + hp[i].n));
+    return 0;
+  }
+  const int np = argc > 2 ? std::atoi(argv[2]) : 42;
+  const int m = argc > 3 ? std::atoi(argv[3]) : 200000;
+  const int n = argc > 4 ? std::atoi(argv[4]) : 200000;
+  if (np < 1 || np > 4096 || m < 1 || m > 1 << 20 || n < 32 || n > 1 << 20) { std::fprintf(stderr, "bad size\n"); return 2; }
+  srand(1);
+  std::string x(m, 'A'), y(n, 'A');
+  for (auto& c : x) c = "ACGT"[rand() & 3];
+  for (auto& c : y) c = "ACGT"[rand() & 3];
+  const HostPair H = build_pair(x, y);
+  for (int i = 0; i < np; ++i) hp.push_back(H);
+  const double ms = run(hp, false, 2, sums, true);
+  const double cells = (double)np * m * n;
+  std::printf("{\"pairs\": %d, \"m\": %d, \"n\": %d, \"bands\": %d, \"ms\": %.2f, \"gcups\": %.1f}\n", np, m, n, H.nb, ms,
+              cells / ms / 1e6);
+  return 0;
+}
