@@ -12,13 +12,16 @@
 // in dependency order (band-major), so a band's producer is always running.
 //
 //   gotoh_chain check < pairs    "x y" per line, any |x|: H[m][n] per pair
-//   gotoh_chain rate [pairs] [m] [n]
-//                                pairs random m x n pairs, prints GCUPS (fill only,
-//                                no traceback stores)
+//   gotoh_chain rate [pairs] [m] [n] [window]
+//                                pairs random m x n pairs, prints GCUPS; window >= 0
+//                                stores the four traceback words of every 4-step
+//                                block within `window` columns of the diagonal
+//                                (4-step blocks of 4 KB), else fill only
 //
 // C5's scoring (pxy 3, go 3, ge 1).  A probe: not part of libnwk.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>
@@ -54,7 +57,9 @@ struct Pair {
   const unsigned* yr;  // [(n >> 5) + 4][2] reversed column chunks (gotoh_gpu.hip)
   u64* hand;           // [nb][nw][kPs] granules of each band's last row
   long long* out;      // sum of v over column n, all rows (atomic)
+  unsigned* mat;       // (STORE) [nb][nblk][1024] traceback words, 4-step blocks
   int m, n, nb, nw;    // nw = (n >> 5) + 1 chunks of 32 columns
+  int w, nblk;         // (STORE) window: steps within w columns of the diagonal j = i n / m
 };
 
 __device__ __forceinline__ u64 opaque_zero() {
@@ -63,7 +68,7 @@ __device__ __forceinline__ u64 opaque_zero() {
   return z;
 }
 
-template <bool CHECK>
+template <bool CHECK, bool STORE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void gotoh_chain(
     const Pair* pairs, const int2* tasks, int ntasks, unsigned* counter, unsigned* err, unsigned epoch,
     unsigned* sink) {
@@ -99,6 +104,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
     for (int q = 0; q < NQ1; ++q) e[q] = f[q] = ~0u;
     const int nsteps = P.n + 2048 + 32;
+    // (STORE) the band's stored 4-step blocks: its diagonal cells lie at steps
+    // R0 n / m .. + 2048 (1 + n / m); keep w columns either side
+    const int blo = STORE ? (int)std::max(0ll, ((long long)R0 * P.n / P.m - P.w) >> 2) : 0;
+    // block layout: word w of step s at w * 256 + (s & 2) * 64 + 2 lane + (s & 1)
+    unsigned* mb = STORE ? P.mat + (size_t)band * P.nblk * 1024 + lane * 2 : nullptr;
+    unsigned dq[4][2];
     long long acc = 0;
     bool ok = true;
     for (int s0 = 0; s0 < nsteps && ok; s0 += 32) {
@@ -192,6 +203,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             }
           }
           sk ^= D;
+          if constexpr (STORE) {  // four words per lane and step; every 2 steps one 8-byte
+                                  // store per word, 512 B contiguous across the wave
+            dq[0][r & 1] = D;
+            dq[1][r & 1] = Fs;
+            dq[2][r & 1] = Ee;
+            dq[3][r & 1] = Fe;
+            if ((r & 1) == 1) {
+              const int rel = (s >> 2) - blo;
+              if ((unsigned)rel < (unsigned)P.nblk) {
+                typedef unsigned u2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+                for (int w4 = 0; w4 < 4; ++w4)
+                  __builtin_nontemporal_store(u2{dq[w4][0], dq[w4][1]},
+                                              reinterpret_cast<u2*>(mb + (size_t)rel * 1024 + w4 * 256 + (s & 2) * 64));
+              }
+            }
+          }
         }
       };
       if (s0 < 2048 + 32) seg(std::true_type{});
@@ -259,7 +287,8 @@ static HostPair build_pair(const std::string& x, const std::string& y) {
 
 // uploads `hp` (shared device copies for identical pairs when `same`), runs
 // `reps` timed launches after one warm-up; returns ms per launch
-static double run(const std::vector<HostPair>& hp, bool check, int reps, std::vector<long long>& out, bool same) {
+static double run(const std::vector<HostPair>& hp, bool check, int reps, std::vector<long long>& out, bool same,
+                  int win = -1) {
   const int np = (int)hp.size();
   std::vector<Pair> P(np);
   std::vector<void*> allocs;
@@ -283,7 +312,14 @@ static double run(const std::vector<HostPair>& hp, bool check, int reps, std::ve
     HIPCHK(hipMalloc(&hand, (size_t)H.nb * nw * kPs * 8));
     HIPCHK(hipMemset(hand, 0, (size_t)H.nb * nw * kPs * 8));
     allocs.push_back(hand);
-    P[i] = Pair{dx, dy, hand, nullptr, H.m, H.n, H.nb, nw};
+    unsigned* mat = nullptr;
+    int nblk = 0;
+    if (win >= 0) {  // blocks covering 2048 (1 + n / m) + 2 win steps, + 2 for rounding
+      nblk = (int)((2048ll * (H.m + H.n) / H.m + 2ll * win) / 4) + 2;
+      HIPCHK(hipMalloc(&mat, (size_t)H.nb * nblk * 1024 * 4));
+      allocs.push_back(mat);
+    }
+    P[i] = Pair{dx, dy, hand, nullptr, mat, H.m, H.n, H.nb, nw, win, nblk};
     maxb = std::max(maxb, H.nb);
   }
   long long* dout;
@@ -316,8 +352,9 @@ static double run(const std::vector<HostPair>& hp, bool check, int reps, std::ve
     HIPCHK(hipMemset(dctr, 0, 4));
     HIPCHK(hipMemset(dout, 0, 8 * np));
     HIPCHK(hipEventRecord(a));
-    if (check) hipLaunchKernelGGL(gotoh_chain<true>, dim3(grid), dim3(256), 0, 0, dp, dt, (int)tk.size(), dctr, derr, 1u + r, dsink);
-    else hipLaunchKernelGGL(gotoh_chain<false>, dim3(grid), dim3(256), 0, 0, dp, dt, (int)tk.size(), dctr, derr, 1u + r, dsink);
+    if (check) hipLaunchKernelGGL((gotoh_chain<true, false>), dim3(grid), dim3(256), 0, 0, dp, dt, (int)tk.size(), dctr, derr, 1u + r, dsink);
+    else if (win >= 0) hipLaunchKernelGGL((gotoh_chain<false, true>), dim3(grid), dim3(256), 0, 0, dp, dt, (int)tk.size(), dctr, derr, 1u + r, dsink);
+    else hipLaunchKernelGGL((gotoh_chain<false, false>), dim3(grid), dim3(256), 0, 0, dp, dt, (int)tk.size(), dctr, derr, 1u + r, dsink);
     HIPCHK(hipEventRecord(b));
     HIPCHK(hipEventSynchronize(b));
     HIPCHK(hipGetLastError());
@@ -354,6 +391,7 @@ int main(int argc, char** argv) {
   const int np = argc > 2 ? std::atoi(argv[2]) : 42;
   const int m = argc > 3 ? std::atoi(argv[3]) : 200000;
   const int n = argc > 4 ? std::atoi(argv[4]) : 200000;
+  const int win = argc > 5 ? std::atoi(argv[5]) : -1;  // >= 0: store the traceback words within win columns
   if (np < 1 || np > 4096 || m < 1 || m > 1 << 20 || n < 32 || n > 1 << 20) { std::fprintf(stderr, "bad size\n"); return 2; }
   srand(1);
   std::string x(m, 'A'), y(n, 'A');
@@ -361,9 +399,9 @@ int main(int argc, char** argv) {
   for (auto& c : y) c = "ACGT"[rand() & 3];
   const HostPair H = build_pair(x, y);
   for (int i = 0; i < np; ++i) hp.push_back(H);
-  const double ms = run(hp, false, 2, sums, true);
+  const double ms = run(hp, false, 2, sums, true, win);
   const double cells = (double)np * m * n;
-  std::printf("{\"pairs\": %d, \"m\": %d, \"n\": %d, \"bands\": %d, \"ms\": %.2f, \"gcups\": %.1f}\n", np, m, n, H.nb, ms,
-              cells / ms / 1e6);
+  std::printf("{\"pairs\": %d, \"m\": %d, \"n\": %d, \"bands\": %d, \"window\": %d, \"ms\": %.2f, \"gcups\": %.1f}\n", np, m, n,
+              H.nb, win, ms, cells / ms / 1e6);
   return 0;
 }
