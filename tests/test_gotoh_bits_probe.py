@@ -107,3 +107,32 @@ def test_gotoh_bits_gpu_chained_bands():
     out = subprocess.run([exe, "check"], input=inp, capture_output=True, text=True, timeout=120, check=True)
     got = [int(v) for v in out.stdout.split()]
     assert got == [oracle.score_affine(x, y, 3, 3, 1) for x, y in prs]
+
+
+@pytest.mark.gpu
+def test_gotoh_bits_gpu_stored_bits_walk():
+    """Fill + store on the GPU, walk on the host: gotoh_chain `trace` stores every
+    cell's four words (D, F-source, E-extend, F-extend) in the probe's 4-step
+    block layout and walks nwo_pair_affine's traceback over them; the strings
+    must equal the oracle's alignment, band edges and ties included."""
+    exe = os.path.join(ROOT, "tools", "probe", "gotoh_chain")
+    assert os.path.exists(exe), "tools/probe/gotoh_chain not built (run __graft_entry__.build())"
+    rng = random.Random(31)
+    prs = []
+    sizes = [(2048, 300), (2049, 2049), (4100, 1000), (1, 700), (3000, 1), (5000, 2200)]
+    for t in range(16):
+        m, n = sizes[t] if t < len(sizes) else (rng.randint(1, 5000), rng.randint(1, 2500))
+        x = "".join(rng.choice("ACGT") for _ in range(m))
+        if t % 3 == 1:
+            y = x[:n] + "".join(rng.choice("ACGT") for _ in range(max(0, n - m)))
+        else:
+            y = "".join(rng.choice("ACGT"[:rng.randint(2, 4)]) for _ in range(n))
+        prs.append((x, y))
+    inp = "".join("%s %s\n" % p for p in prs)
+    out = subprocess.run([exe, "trace"], input=inp, capture_output=True, text=True, timeout=120, check=True)
+    lines = out.stdout.splitlines()
+    assert len(lines) == len(prs)
+    for (x, y), line in zip(prs, lines):
+        h, a1, a2 = line.split()
+        pen, e1, e2 = oracle.pair_affine(x, y, 3, 3, 1)
+        assert (int(h), a1.encode(), a2.encode()) == (pen, e1, e2), (len(x), len(y))

@@ -12,6 +12,8 @@
 // in dependency order (band-major), so a band's producer is always running.
 //
 //   gotoh_chain check < pairs    "x y" per line, any |x|: H[m][n] per pair
+//   gotoh_chain trace < pairs    the same with every cell's four words stored, then
+//                                nwo_pair_affine's walk over them on the host: "H a1 a2"
 //   gotoh_chain rate [pairs] [m] [n] [window]
 //                                pairs random m x n pairs, prints GCUPS; window >= 0
 //                                stores the four traceback words of every 4-step
@@ -288,7 +290,7 @@ static HostPair build_pair(const std::string& x, const std::string& y) {
 // uploads `hp` (shared device copies for identical pairs when `same`), runs
 // `reps` timed launches after one warm-up; returns ms per launch
 static double run(const std::vector<HostPair>& hp, bool check, int reps, std::vector<long long>& out, bool same,
-                  int win = -1) {
+                  int win = -1, std::vector<std::vector<unsigned>>* mats = nullptr, std::vector<int>* nblks = nullptr) {
   const int np = (int)hp.size();
   std::vector<Pair> P(np);
   std::vector<void*> allocs;
@@ -352,7 +354,8 @@ static double run(const std::vector<HostPair>& hp, bool check, int reps, std::ve
     HIPCHK(hipMemset(dctr, 0, 4));
     HIPCHK(hipMemset(dout, 0, 8 * np));
     HIPCHK(hipEventRecord(a));
-    if (check) hipLaunchKernelGGL((gotoh_chain<true, false>), dim3(grid), dim3(256), 0, 0, dp, dt, (int)tk.size(), dctr, derr, 1u + r, dsink);
+    if (check && win >= 0) hipLaunchKernelGGL((gotoh_chain<true, true>), dim3(grid), dim3(256), 0, 0, dp, dt, (int)tk.size(), dctr, derr, 1u + r, dsink);
+    else if (check) hipLaunchKernelGGL((gotoh_chain<true, false>), dim3(grid), dim3(256), 0, 0, dp, dt, (int)tk.size(), dctr, derr, 1u + r, dsink);
     else if (win >= 0) hipLaunchKernelGGL((gotoh_chain<false, true>), dim3(grid), dim3(256), 0, 0, dp, dt, (int)tk.size(), dctr, derr, 1u + r, dsink);
     else hipLaunchKernelGGL((gotoh_chain<false, false>), dim3(grid), dim3(256), 0, 0, dp, dt, (int)tk.size(), dctr, derr, 1u + r, dsink);
     HIPCHK(hipEventRecord(b));
@@ -367,25 +370,82 @@ static double run(const std::vector<HostPair>& hp, bool check, int reps, std::ve
   if (herr) { std::fprintf(stderr, "gotoh_chain: wait timed out (err %u)\n", herr); std::exit(4); }
   out.resize(np);
   HIPCHK(hipMemcpy(out.data(), dout, 8 * np, hipMemcpyDeviceToHost));
+  if (mats && win >= 0) {  // the stored words, per pair
+    mats->resize(np);
+    nblks->resize(np);
+    for (int i = 0; i < np; ++i) {
+      (*nblks)[i] = P[i].nblk;
+      (*mats)[i].resize((size_t)hp[i].nb * P[i].nblk * 1024);
+      HIPCHK(hipMemcpy((*mats)[i].data(), P[i].mat, (*mats)[i].size() * 4, hipMemcpyDeviceToHost));
+    }
+  }
   for (void* p : allocs) (void)hipFree(p);
   (void)hipFree(dout); (void)hipFree(dp); (void)hipFree(dt); (void)hipFree(dctr); (void)hipFree(derr); (void)hipFree(dsink);
   return reps > 0 ? ms_sum / reps : 0.0;
+}
+
+// nwo_pair_affine's walk (oracle/nw_oracle.c:240-270) over the words the GPU
+// stored: cell (i, j) is row r = i - 1 of band r / 2048 (lane t, bit b), step
+// s = j + 32 t + b, word w at block (s >> 2) - blo, w * 256 + (s & 2) * 64 + 2 t + (s & 1)
+static void walk_stored(const std::string& x, const std::string& y, const std::vector<unsigned>& mat, int nblk,
+                        int win, std::string& a1, std::string& a2) {
+  const int m = (int)x.size(), n = (int)y.size(), l = m + n;
+  auto bits = [&](int i, int j) {
+    const int r = i - 1, band = r / 2048, t = (r % 2048) / 32, b = r % 32, s = j + 32 * t + b;
+    const long long blo = std::max(0ll, ((long long)band * 2048 * n / m - win) >> 2);
+    const long long rel = (s >> 2) - blo;
+    if (rel < 0 || rel >= nblk) { std::fprintf(stderr, "walk left the stored blocks\n"); std::exit(5); }
+    const size_t base = ((size_t)band * nblk + rel) * 1024 + (s & 2) * 64 + 2 * t + (s & 1);
+    unsigned o = 0;
+    for (int w = 0; w < 4; ++w) o |= ((mat[base + w * 256] >> b) & 1u) << w;
+    return o;  // bit 0 D, 1 F-source, 2 E-extend, 3 F-extend
+  };
+  std::string xa(l + 1, ' '), ya(l + 1, ' ');
+  int i = m, j = n, xp = l, yp = l, st = 0;
+  while (!(i == 0 || j == 0)) {
+    const unsigned c = bits(i, j);
+    if (st == 0) {
+      if (c & 1u) { xa[xp--] = x[i - 1]; ya[yp--] = y[j - 1]; --i; --j; continue; }
+      st = (c & 2u) ? 1 : 2;
+    }
+    if (st == 1) { st = (c & 8u) ? 1 : 0; xa[xp--] = x[i - 1]; ya[yp--] = '_'; --i; }
+    else { st = (c & 4u) ? 2 : 0; xa[xp--] = '_'; ya[yp--] = y[j - 1]; --j; }
+  }
+  while (xp > 0) xa[xp--] = i > 0 ? x[--i] : '_';
+  while (yp > 0) ya[yp--] = j > 0 ? y[--j] : '_';
+  int id = 1;
+  for (int a = l; a >= 1; --a)
+    if (ya[a] == '_' && xa[a] == '_') { id = a + 1; break; }
+  a1 = xa.substr(id);
+  a2 = ya.substr(id);
 }
 
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "rate";
   std::vector<HostPair> hp;
   std::vector<long long> sums;
-  if (mode == "check") {
-    std::vector<std::pair<int, int>> mn;
+  if (mode == "check" || mode == "trace") {
+    std::vector<std::pair<std::string, std::string>> seqs;
     std::string x, y;
+    int maxlen = 0;
     while (std::cin >> x >> y) {
       if (x.empty() || y.empty() || x.size() > (1u << 20) || y.size() > (1u << 20)) { std::fprintf(stderr, "bad pair\n"); return 2; }
       hp.push_back(build_pair(x, y));
+      seqs.emplace_back(x, y);
+      maxlen = std::max(maxlen, (int)y.size());
     }
-    run(hp, true, 0, sums, false);
-    for (size_t i = 0; i < hp.size(); ++i)  // H = G(0, n) - sum v + (m + n) ge
-      std::printf("%lld\n", kGO - sums[i] + (long long)(hp[i].m + hp[i].n));
+    // trace: every step stored (window wider than any pair), walked on the host
+    const int win = mode == "trace" ? maxlen + 2048 : -1;
+    std::vector<std::vector<unsigned>> mats;
+    std::vector<int> nblks;
+    run(hp, true, 0, sums, false, win, &mats, &nblks);
+    for (size_t i = 0; i < hp.size(); ++i) {  // H = G(0, n) - sum v + (m + n) ge
+      const long long H = kGO - sums[i] + (long long)(hp[i].m + hp[i].n);
+      if (mode == "check") { std::printf("%lld\n", H); continue; }
+      std::string a1, a2;
+      walk_stored(seqs[i].first, seqs[i].second, mats[i], nblks[i], win, a1, a2);
+      std::printf("%lld %s %s\n", H, a1.empty() ? "-" : a1.c_str(), a2.empty() ? "-" : a2.c_str());
+    }
     return 0;
   }
   const int np = argc > 2 ? std::atoi(argv[2]) : 42;
