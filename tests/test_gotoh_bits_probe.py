@@ -136,3 +136,30 @@ def test_gotoh_bits_gpu_stored_bits_walk():
         h, a1, a2 = line.split()
         pen, e1, e2 = oracle.pair_affine(x, y, 3, 3, 1)
         assert (int(h), a1.encode(), a2.encode()) == (pen, e1, e2), (len(x), len(y))
+
+
+@pytest.mark.gpu
+def test_gotoh_bits_gpu_device_walk():
+    """Fill, store and walk all on the GPU (gotoh_chain `dtrace`: gotoh_walk, one
+    wave per pair over LDS tiles of the stored words): the alignments equal the
+    oracle's.  The probe's walk buffer wants pairs of equal m + n."""
+    exe = os.path.join(ROOT, "tools", "probe", "gotoh_chain")
+    assert os.path.exists(exe), "tools/probe/gotoh_chain not built (run __graft_entry__.build())"
+    rng = random.Random(37)
+    prs = []
+    for t, m in enumerate([2048, 2049, 4097, 1, 5999, 3000, 100, 4500, 2500, 5000, 1500, 3500]):
+        n = 6000 - m
+        x = "".join(rng.choice("ACGT") for _ in range(m))
+        if t % 3 == 1:
+            y = x[:n] + "".join(rng.choice("ACGT") for _ in range(max(0, n - m)))
+        else:
+            y = "".join(rng.choice("ACGT"[:rng.randint(2, 4)]) for _ in range(n))
+        prs.append((x, y))
+    inp = "".join("%s %s\n" % p for p in prs)
+    out = subprocess.run([exe, "dtrace"], input=inp, capture_output=True, text=True, timeout=120, check=True)
+    lines = out.stdout.splitlines()
+    assert len(lines) == len(prs)
+    for (x, y), line in zip(prs, lines):
+        h, a1, a2 = line.split()
+        pen, e1, e2 = oracle.pair_affine(x, y, 3, 3, 1)
+        assert (int(h), a1.encode(), a2.encode()) == (pen, e1, e2), (len(x), len(y))

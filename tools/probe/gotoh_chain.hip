@@ -14,6 +14,10 @@
 //   gotoh_chain check < pairs    "x y" per line, any |x|: H[m][n] per pair
 //   gotoh_chain trace < pairs    the same with every cell's four words stored, then
 //                                nwo_pair_affine's walk over them on the host: "H a1 a2"
+//   gotoh_chain dtrace < pairs   the same walk on the device (gotoh_walk; pairs of
+//                                equal m + n)
+//   gotoh_chain dtrate [pairs] [m] [n] [window]
+//                                fill + windowed store, then the device walk, timed
 //   gotoh_chain rate [pairs] [m] [n] [window]
 //                                pairs random m x n pairs, prints GCUPS; window >= 0
 //                                stores the four traceback words of every 4-step
@@ -249,6 +253,82 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   sink[(blockIdx.x * 4 + wid) * 64 + lane] = sk;
 }
 
+// Device walk (probe): one wave per pair walks nwo_pair_affine's traceback
+// over the stored words.  Tiles of 64 steps x 2 row-lanes (t0 - 1, t0) of one
+// band are staged in LDS by the whole wave (lane L: step s_hi - L, 8 loads),
+// then every lane runs the same (uniform) walk over the tile; lane 0 writes
+// the moves ('D', 'U', 'L' from the end) and the walk's last cell.
+__global__ __launch_bounds__(64) void gotoh_walk(const Pair* pairs, int np, char* moves, int* nmoves, int2* ends,
+                                                 unsigned* err) {
+  __shared__ unsigned tile[4][2][64];
+  const int pi = blockIdx.x;
+  if (pi >= np) return;
+  const int lane = threadIdx.x;
+  const Pair P = pairs[pi];
+  char* mv = moves + (size_t)pi * (P.m + P.n);
+  int i = P.m, j = P.n, st = 0, k = 0;
+  int tb = -1, t0 = -1, shi = -1;  // the staged tile
+  long long tblo = 0;                // its band's first stored block
+  while (i > 0 && j > 0) {
+    const int r = i - 1, band = r >> 11, t = (r & 2047) >> 5, b = r & 31, s = j + 32 * t + b;
+    if (band != tb || (t != t0 && t != t0 - 1) || s > shi || s < shi - 63) {
+      tb = band;
+      t0 = t;
+      shi = s;
+      const long long blo = std::max(0ll, ((long long)band * 2048 * P.n / P.m - P.w) >> 2);
+      tblo = blo;
+      const int ss = shi - lane;
+      const long long rel = ss >= 0 ? (ss >> 2) - blo : -1;
+      const bool in = rel >= 0 && rel < P.nblk;
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int tl = t0 - 1 + h;
+          unsigned val = 0;
+          if (in && tl >= 0)
+            val = P.mat[((size_t)band * P.nblk + rel) * 1024 + w * 256 + (ss & 2) * 64 + 2 * tl + (ss & 1)];
+          tile[w][h][lane] = val;
+        }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __syncthreads();
+    }
+    {  // a cell outside the stored blocks (the path left the window) fails the walk
+      const long long rel0 = (s >> 2) - tblo;
+      if (rel0 < 0 || rel0 >= P.nblk) {
+        if (lane == 0) atomicOr(err, 2u);
+        break;
+      }
+    }
+    const int h = t == t0 ? 1 : 0, q = shi - s;
+    const unsigned c = ((tile[0][h][q] >> b) & 1u) | ((tile[1][h][q] >> b) & 1u) << 1 |
+                       ((tile[2][h][q] >> b) & 1u) << 2 | ((tile[3][h][q] >> b) & 1u) << 3;
+    char m;
+    if (st == 0 && (c & 1u)) {
+      m = 'D';
+      --i;
+      --j;
+    } else {
+      if (st == 0) st = (c & 2u) ? 1 : 2;
+      if (st == 1) {
+        st = (c & 8u) ? 1 : 0;
+        m = 'U';
+        --i;
+      } else {
+        st = (c & 4u) ? 2 : 0;
+        m = 'L';
+        --j;
+      }
+    }
+    if (lane == 0) mv[k] = m;
+    ++k;
+  }
+  if (lane == 0) {
+    nmoves[pi] = k;
+    ends[pi] = make_int2(i, j);
+  }
+}
+
 static int code(char c) { return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : 3; }
 
 struct HostPair {
@@ -289,8 +369,16 @@ static HostPair build_pair(const std::string& x, const std::string& y) {
 
 // uploads `hp` (shared device copies for identical pairs when `same`), runs
 // `reps` timed launches after one warm-up; returns ms per launch
+struct Walks {
+  std::vector<std::string> moves;  // from the end of the alignment
+  std::vector<int> n;
+  std::vector<int2> end;
+  float ms = 0;
+};
+
 static double run(const std::vector<HostPair>& hp, bool check, int reps, std::vector<long long>& out, bool same,
-                  int win = -1, std::vector<std::vector<unsigned>>* mats = nullptr, std::vector<int>* nblks = nullptr) {
+                  int win = -1, std::vector<std::vector<unsigned>>* mats = nullptr, std::vector<int>* nblks = nullptr,
+                  Walks* walks = nullptr) {
   const int np = (int)hp.size();
   std::vector<Pair> P(np);
   std::vector<void*> allocs;
@@ -370,6 +458,40 @@ static double run(const std::vector<HostPair>& hp, bool check, int reps, std::ve
   if (herr) { std::fprintf(stderr, "gotoh_chain: wait timed out (err %u)\n", herr); std::exit(4); }
   out.resize(np);
   HIPCHK(hipMemcpy(out.data(), dout, 8 * np, hipMemcpyDeviceToHost));
+  if (walks && win >= 0) {  // device walk over the stored words, one wave per pair
+    char* dmv;
+    int* dnm;
+    int2* den;
+    size_t tot = 0;
+    for (const HostPair& H : hp) tot += (size_t)H.m + H.n;
+    HIPCHK(hipMalloc(&dmv, tot));
+    HIPCHK(hipMalloc(&dnm, 4 * np));
+    HIPCHK(hipMalloc(&den, 8 * np));
+    std::vector<size_t> off(np + 1, 0);
+    for (int i = 0; i < np; ++i) off[i + 1] = off[i] + (size_t)hp[i].m + hp[i].n;
+    // (the kernel indexes moves by pi * (m + n): equal-size pairs only, checked here)
+    for (int i = 0; i < np; ++i)
+      if (off[i] != (size_t)i * ((size_t)hp[i].m + hp[i].n)) { std::fprintf(stderr, "dtrace: pairs must share m + n\n"); std::exit(2); }
+    HIPCHK(hipEventRecord(a));
+    hipLaunchKernelGGL(gotoh_walk, dim3(np), dim3(64), 0, 0, dp, np, dmv, dnm, den, derr);
+    HIPCHK(hipEventRecord(b));
+    HIPCHK(hipEventSynchronize(b));
+    HIPCHK(hipGetLastError());
+    float wms = 0;
+    HIPCHK(hipEventElapsedTime(&wms, a, b));
+    walks->ms = wms;
+    HIPCHK(hipMemcpy(&herr, derr, 4, hipMemcpyDeviceToHost));
+    if (herr) { std::fprintf(stderr, "gotoh_walk: left the stored window (err %u)\n", herr); std::exit(5); }
+    std::vector<char> mv(tot);
+    walks->n.resize(np);
+    walks->end.resize(np);
+    HIPCHK(hipMemcpy(mv.data(), dmv, tot, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(walks->n.data(), dnm, 4 * np, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(walks->end.data(), den, 8 * np, hipMemcpyDeviceToHost));
+    walks->moves.resize(np);
+    for (int i = 0; i < np; ++i) walks->moves[i].assign(mv.data() + off[i], mv.data() + off[i] + walks->n[i]);
+    (void)hipFree(dmv); (void)hipFree(dnm); (void)hipFree(den);
+  }
   if (mats && win >= 0) {  // the stored words, per pair
     mats->resize(np);
     nblks->resize(np);
@@ -424,6 +546,70 @@ int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "rate";
   std::vector<HostPair> hp;
   std::vector<long long> sums;
+  if (mode == "dtrace" || mode == "dtrate") {
+    // dtrace: stdin pairs (equal m + n), every step stored, walked on the device
+    // dtrate [pairs] [m] [n] [window]: C5-shaped random pairs, fill + store, then
+    // the device walk; prints both times
+    std::vector<std::pair<std::string, std::string>> seqs;
+    int win;
+    if (mode == "dtrace") {
+      std::string x, y;
+      int maxlen = 0;
+      while (std::cin >> x >> y) {
+        hp.push_back(build_pair(x, y));
+        seqs.emplace_back(x, y);
+        maxlen = std::max(maxlen, (int)y.size());
+      }
+      if (hp.empty()) return 2;
+      win = maxlen + 2048;
+    } else {
+      const int np = argc > 2 ? std::atoi(argv[2]) : 16;
+      const int m = argc > 3 ? std::atoi(argv[3]) : 200000;
+      const int n = argc > 4 ? std::atoi(argv[4]) : 200000;
+      win = argc > 5 ? std::atoi(argv[5]) : 8192;
+      if (np < 1 || np > 512 || m < 2048 || m > 1 << 20 || n < 32 || n > 1 << 20 || win < 0) return 2;
+      srand(3);
+      for (int q = 0; q < np; ++q) {  // related pairs: a mutated copy (the path stays near the diagonal)
+        std::string x(m, 'A'), y;
+        for (auto& c : x) c = "ACGT"[rand() & 3];
+        y = x.substr(0, std::min(m, n));
+        for (auto& c : y) if ((rand() & 7) == 0) c = "ACGT"[rand() & 3];
+        while ((int)y.size() < n) y.push_back("ACGT"[rand() & 3]);
+        hp.push_back(build_pair(x, y));
+      }
+    }
+    Walks wk;
+    const double ms = run(hp, mode == "dtrace", mode == "dtrace" ? 0 : 1, sums, false, win, nullptr, nullptr, &wk);
+    if (mode == "dtrate") {
+      long long mv = 0;
+      for (int v : wk.n) mv += v;
+      std::printf("{\"pairs\": %d, \"m\": %d, \"n\": %d, \"window\": %d, \"fill_store_ms\": %.2f, \"walk_ms\": %.2f, "
+                  "\"moves\": %lld, \"ns_per_move_per_pair\": %.1f}\n",
+                  (int)hp.size(), hp[0].m, hp[0].n, win, ms, wk.ms, mv, wk.ms * 1e6 / (mv / (double)hp.size()));
+      return 0;
+    }
+    for (size_t q = 0; q < hp.size(); ++q) {
+      const std::string &x = seqs[q].first, &y = seqs[q].second;
+      const int m = (int)x.size(), n = (int)y.size(), l = m + n;
+      std::string xa(l + 1, ' '), ya(l + 1, ' ');
+      int i = m, j = n, xp = l, yp = l;
+      for (char c : wk.moves[q]) {
+        if (c == 'D') { xa[xp--] = x[i - 1]; ya[yp--] = y[j - 1]; --i; --j; }
+        else if (c == 'U') { xa[xp--] = x[i - 1]; ya[yp--] = '_'; --i; }
+        else { xa[xp--] = '_'; ya[yp--] = y[j - 1]; --j; }
+      }
+      if (i != wk.end[q].x || j != wk.end[q].y) { std::fprintf(stderr, "dtrace: end cell mismatch\n"); return 6; }
+      while (xp > 0) xa[xp--] = i > 0 ? x[--i] : '_';
+      while (yp > 0) ya[yp--] = j > 0 ? y[--j] : '_';
+      int id = 1;
+      for (int a = l; a >= 1; --a)
+        if (ya[a] == '_' && xa[a] == '_') { id = a + 1; break; }
+      const long long H = kGO - sums[q] + (long long)(m + n);
+      std::printf("%lld %s %s\n", H, xa.substr(id).empty() ? "-" : xa.substr(id).c_str(),
+                  ya.substr(id).empty() ? "-" : ya.substr(id).c_str());
+    }
+    return 0;
+  }
   if (mode == "check" || mode == "trace") {
     std::vector<std::pair<std::string, std::string>> seqs;
     std::string x, y;
