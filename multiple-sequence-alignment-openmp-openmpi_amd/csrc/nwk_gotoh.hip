@@ -1,0 +1,460 @@
+// nwk_gotoh.hip -- nw_align_gotoh: the affine-gap variant (the
+// build defines it, oracle/nw_oracle.c nwo_pair_affine restates it) as
+// bit-sliced thermometer planes, one bit per DP cell.
+//
+// The step (nwk_gotoh_planes.h) works in G-space (ge subtracted per step)
+// relative to G_diag: a difference v / h in [-go, go + 2 ge] is held as
+// 2 (go + ge) planes, a gap offset min(e, go) / min(f, go) as go planes, and
+// every output plane is an OR of (plane AND NOT plane) terms -- one
+// v_bitop3_b32 per term for 32 cells.  C5's scoring (pxy 3, go 3, ge 1) is
+// ~175 VALU per wave-step for 32 cells against nw_align_pka's ~7.4 per cell.
+//
+// Layout (nw_align_bits' anti-diagonal bands): a wave owns a 2048-row band;
+// bit b of lane t is row R0 + 32 t + b + 1 at (1-based) column s - 32 t - b at
+// step s.  A cell's left neighbour is the same bit one step earlier; its upper
+// neighbour is the bit below one step earlier (a 1-bit funnel shift with lane
+// t - 1's top bit through DPP wave_shr:1).  Lane 0 bit 0 reads the band
+// above's last row: that row (lane 63 bit 31, column s - 2047) goes to an LDS
+// ring each step, and at the end of every 32-step segment its next complete
+// 32 columns are packed by ballot into one word per h / f plane and published
+// as self-tagged granules {epoch:32 | word:32}, which the band below polls
+// with atomic reads (the coherence point: a plain load can hit a stale line in
+// the reading XCD's L2) and stages in LDS as the DPP fill-in of lane 0.
+//
+// Storage: four words per lane and step -- D (X == S: the diagonal candidate
+// is the minimum), F-source (f == 0: H came from F), E-extend (eL < go) and
+// F-extend (fU < go), exactly the decisions of nwo_pair_affine's walk
+// (oracle/nw_oracle.c:240-256) -- in 4-step blocks of 4 KB, one 8-byte store
+// per word every two steps (512 B contiguous across the wave), only the
+// blocks within bits_w columns of the diagonal when windowed.
+//
+// Traceback: the wave that finishes a pair's last band walks the three-state
+// walk from (m, n) on the scalar unit over tiles of 64 steps x 128 rows held
+// in VGPRs (lane L = step 32 k + L, four row-lanes x four words), one
+// v_readlane per word per move; a gap's first column is emitted as 'u' / 'l'
+// (the finalize charges go + ge there, ge elsewhere).  A cell outside the
+// stored blocks flags the pair for a wider re-run (FillArgs::retry).
+#include "nwk_bits_dev.h"
+#include "nwk_gotoh_planes.h"
+
+namespace nwk {
+namespace {
+
+using namespace gotoh_bits;
+
+template <class C>
+struct GGeo {
+  static constexpr int NQ1 = C::NQ > 0 ? C::NQ : 1;  // gap-offset planes held (go = 0: one dummy)
+  static constexpr int kPl = C::NV + C::NQ;          // planes handed down: h, then f
+  static constexpr int kPs = (kPl + 3) & ~3;         // LDS / granule stride per column / chunk
+  static_assert(kPl <= 64, "one granule per lane");
+};
+
+// At least NWK_GOTOH_WPE waves per SIMD: the step is issue-bound and a lone
+// wave issues a VALU op only every ~8 cycles, so occupancy is
+// what fills the SIMD; the probe's step needed 104-117 VGPRs (4 waves fit).
+#ifndef NWK_GOTOH_WPE
+#define NWK_GOTOH_WPE 4
+#endif
+
+// ---- traceback ---------------------------------------------------------------
+
+struct Walk {
+  int i, j, st, k;  // cell, state (0 H, 1 F, 2 E), moves emitted
+  int b, q;         // bit of the cell's row in its row-lane, tile lane of its step
+  unsigned acc;     // moves (k & ~3) .. k - 1, one byte each
+};
+
+// one move out of the walk: byte k of the reversed move string (flushed 256 B
+// at a time from the VGPR outv, one dword per lane)
+__device__ __forceinline__ void walk_emit(Walk& w, unsigned mv, unsigned& outv, unsigned* ops, int lane) {
+  w.acc |= mv << (8 * (w.k & 3));
+  if ((w.k & 3) == 3) {
+    outv = lane == ((w.k >> 2) & 63) ? w.acc : outv;
+    w.acc = 0;
+    if ((w.k & 255) == 255) ops[(int64_t)(w.k >> 8) * 64 + lane] = outv;
+  }
+  ++w.k;
+}
+
+// Moves inside row-lane H of the tile (oracle/nw_oracle.c:241-256): returns when
+// the walk reaches row or column 0, leaves the row-lane (b < 0) or the tile's
+// steps (q < qmin), or has emitted kcap moves.
+template <int H>
+__device__ __forceinline__ void walk_rl(const unsigned (&tw)[4][4], Walk& w, int qmin, int kcap, unsigned& outv,
+                                        unsigned* ops, int lane) {
+  for (;;) {
+    if (w.i == 0 || w.j == 0 || w.q < qmin || w.k >= kcap) return;
+    const unsigned dD = (unsigned)__builtin_amdgcn_readlane((int)tw[H][0], w.q);
+    const unsigned dF = (unsigned)__builtin_amdgcn_readlane((int)tw[H][1], w.q);
+    unsigned mv;
+    if (w.st == 0 && ((dD >> w.b) & 1u)) {
+      mv = 'D';
+      --w.i;
+      --w.j;
+      --w.b;
+      w.q -= 2;
+    } else {
+      if (w.st == 0) w.st = ((dF >> w.b) & 1u) ? 1 : 2;
+      if (w.st == 1) {  // F: an UP move; back to H where the gap opened (open wins ties)
+        const unsigned dX = (unsigned)__builtin_amdgcn_readlane((int)tw[H][3], w.q);
+        const bool ext = (dX >> w.b) & 1u;
+        mv = ext ? 'U' : 'u';
+        w.st = ext ? 1 : 0;
+        --w.i;
+        --w.b;
+        --w.q;
+      } else {  // E: a LEFT move
+        const unsigned dE = (unsigned)__builtin_amdgcn_readlane((int)tw[H][2], w.q);
+        const bool ext = (dE >> w.b) & 1u;
+        mv = ext ? 'L' : 'l';
+        w.st = ext ? 2 : 0;
+        --w.j;
+        --w.q;
+      }
+    }
+    walk_emit(w, mv, outv, ops, lane);
+    if (w.b < 0) return;
+  }
+}
+
+__device__ __noinline__ void trace_gotoh(const FillArgs& a, const PairDesc& pd, int lane) {
+  Walk w{pd.m, pd.n, 0, 0, 0, 0, 0u};
+  unsigned outv = 0;
+  unsigned* ops = reinterpret_cast<unsigned*>(a.ops + pd.ops_off);
+  const int nblk = pd.bits_nblk, kcap = pd.m + pd.n;
+  unsigned tw[4][4];
+  int tband = -1, tgrp = 0, tk = 0, slo = 0, shi = -1;
+  bool out = false;
+  while (w.i > 0 && w.j > 0 && w.k < kcap) {
+    const int r = w.i - 1, band = r >> 11, rl = r & (kBR - 1), t = rl >> 5, s = w.j + rl;
+    if (band != tband || (t >> 2) != tgrp || s < 32 * tk || s > 32 * tk + 63) {
+      // tile: steps 32 tk .. + 63 (the cell in its upper half), row-lanes 4 tgrp .. + 3
+      tband = band;
+      tgrp = t >> 2;
+      tk = s >= 64 ? (s >> 5) - 1 : 0;
+      const int blo = gotoh_blk_lo(band, pd.m, pd.n, pd.bits_w);
+      slo = 4 * blo;
+      shi = 4 * (blo + nblk) - 1;
+      const int ss = 32 * tk + lane, rel = (ss >> 2) - blo;
+      if ((unsigned)rel < (unsigned)nblk) {
+        const unsigned* bp = a.mat + pd.mat_off + ((int64_t)band * nblk + rel) * 1024 + (ss & 2) * 64 + 8 * tgrp;
+        const bool od = (ss & 1) != 0;
+#pragma unroll
+        for (int wd = 0; wd < 4; ++wd) {
+          const uint4 p0 = *reinterpret_cast<const uint4*>(bp + wd * 256);
+          const uint4 p1 = *reinterpret_cast<const uint4*>(bp + wd * 256 + 4);
+          tw[0][wd] = od ? p0.y : p0.x;
+          tw[1][wd] = od ? p0.w : p0.z;
+          tw[2][wd] = od ? p1.y : p1.x;
+          tw[3][wd] = od ? p1.w : p1.z;
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+#pragma unroll
+          for (int wd = 0; wd < 4; ++wd) tw[h][wd] = 0u;
+      }
+    }
+    if (s < slo || s > shi) {  // the path left the stored window
+      out = true;
+      break;
+    }
+    w.b = rl & 31;
+    w.q = s - 32 * tk;
+    const int qmin = slo > 32 * tk ? slo - 32 * tk : 0;
+    switch (t & 3) {
+      case 0: walk_rl<0>(tw, w, qmin, kcap, outv, ops, lane); break;
+      case 1: walk_rl<1>(tw, w, qmin, kcap, outv, ops, lane); break;
+      case 2: walk_rl<2>(tw, w, qmin, kcap, outv, ops, lane); break;
+      default: walk_rl<3>(tw, w, qmin, kcap, outv, ops, lane); break;
+    }
+  }
+  const bool bad = !out && w.i > 0 && w.j > 0;  // more moves than m + n: inconsistent words
+  if (bad && lane == 0) atomicOr(a.err, 16u);
+  if (w.k & 3) outv = lane == ((w.k >> 2) & 63) ? w.acc : outv;
+  if ((w.k & 255) && lane < (((w.k & 255) + 3) >> 2)) ops[(int64_t)(w.k >> 8) * 64 + lane] = outv;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) {
+    a.oplen[pd.slot] = out ? 0 : w.k;
+    a.endij[pd.slot] = out ? make_int2(pd.m, pd.n) : make_int2(w.i, w.j);
+    if (out) a.retry[pd.slot] = 1;
+  }
+}
+
+// ---- fill ----------------------------------------------------------------------
+
+template <int PXY, int GO, int GE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_WPE))) void nw_align_gotoh(FillArgs a) {
+  using C = Cfg<GO, GE, PXY>;
+  using G = GGeo<C>;
+  constexpr int NV = C::NV, NQ1 = G::NQ1, kPl = G::kPl, kPs = G::kPs;
+  __shared__ __attribute__((aligned(16))) unsigned cons_all[4][32 * kPs];
+  __shared__ __attribute__((aligned(16))) unsigned ring_all[4][64 * kPs];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  unsigned* cons = cons_all[wid];
+  unsigned* ring = ring_all[wid];
+  for (;;) {
+    unsigned tk = 0;
+    if (lane == 0) tk = atomicAdd(a.counter, 1u);
+    tk = __builtin_amdgcn_readfirstlane(tk);
+    if (tk >= (unsigned)a.ntasks) return;
+    // wave-uniform exit (a per-lane load would make the task loop divergent)
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)a.err, BITS_RLX)) != 0u) return;
+    const int2 task = a.tasks[tk];
+    const PairDesc pd = a.pairs[task.x];
+    const int band = task.y;
+    const int R0 = band * kBR;
+    // code bit planes of rows R0 + 32 lane + b (rows past m: code 0, never traced)
+    unsigned x0 = 0, x1 = 0;
+    {
+      const int base = R0 + 32 * lane;
+      const int nv = pd.m - base;
+      const uint8_t* xc = a.codes + pd.x_off + base;
+#pragma unroll
+      for (int b = 0; b < 32; ++b) {
+        const unsigned cd = b < nv ? (unsigned)xc[b] : 0u;
+        x0 |= (cd & 1u) << b;
+        x1 |= ((cd >> 1) & 1u) << b;
+      }
+    }
+    const int kmax = pd.n >> 5;  // last 32-column chunk holding a real column
+    const int nw = kmax + 1;
+    const bool from_above = band > 0, to_below = band + 1 < pd.nbands;
+    const u64* gin = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)(from_above ? band - 1 : 0) * nw * kPs;
+    u64* gout = a.bnd + pd.bnd_off + (int64_t)band * nw * kPs;
+    const bool gl = lane < kPl;
+    u64 g = 0;
+    if (from_above && gl) g = __hip_atomic_load((gu64*)(gin + lane), BITS_RLX);
+    // left border: v(1, 0) = -go (row 1 only), v(i > 1, 0) = 0; e = +inf (saturated)
+    uint32_t v[NV], e[NQ1], h[NV], f[NQ1];
+    const uint32_t row1 = (band == 0 && lane == 0) ? 1u : 0u;
+#pragma unroll
+    for (int p = 0; p < NV; ++p) {
+      v[p] = p < GO ? ~row1 : 0u;
+      h[p] = 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ1; ++q) e[q] = f[q] = C::NQ > 0 ? ~0u : 0u;
+    // storage: the band's 4-step blocks blo .. blo + nblk (all of them when not windowed)
+    const int nblk = pd.bits_nblk, blo = gotoh_blk_lo(band, pd.m, pd.n, pd.bits_w);
+    unsigned* mb = a.mat + pd.mat_off + (int64_t)band * nblk * 1024 + lane * 2;
+    // y windows: chunk q (columns 32 q .. 32 q + 31) is y position 32 q - 1; at
+    // segment j lane t takes chunk j - t (lo) and chunk j - t - 1 (hi)
+    const unsigned* ywp = a.yw + 2 * (pd.e_off - 1 - 32 * (int64_t)lane);
+    unsigned hi0 = ywp[-64], hi1 = ywp[-63], lo0 = ywp[0], lo1 = ywp[1];
+    const int nseg = kmax + 65;  // the last chunk is published after segment kmax + 64
+    bool ok = true;
+    for (int j = 0; j < nseg; ++j) {
+      // --- the row above for lane 0's columns 32 j .. 32 j + 31 -> cons (bit 31 per column)
+      {
+        unsigned w = 0;  // lane p < kPl: plane p's word (bit r = column 32 j + r)
+        if (!from_above) {
+          // row 0: h(0, 1) = -go (no plane set), h(0, c > 1) = 0 (planes < go), f = +inf
+          const unsigned h0 = j == 0 ? ~3u : ~0u;  // (columns 0 and 1 cleared in chunk 0)
+          w = lane < GO ? h0 : (lane < NV ? 0u : ~0u);
+        } else if (j <= kmax) {
+          if (!__all(!gl || (unsigned)(g >> 32) == a.epoch)) {
+            g = bits_wait(gin + (int64_t)j * kPs + lane, gl, a.epoch, g, a.err);
+            if (!__all(!gl || (unsigned)(g >> 32) == a.epoch)) {
+              ok = false;
+              break;
+            }
+          }
+          w = (unsigned)g;
+          if (j < kmax && gl) g = __hip_atomic_load((gu64*)(gin + (int64_t)(j + 1) * kPs + lane), BITS_RLX);
+        }
+        unsigned ev[kPs];
+#pragma unroll
+        for (int p = 0; p < kPs; ++p)
+          ev[p] = p < kPl ? (((unsigned)__builtin_amdgcn_readlane((int)w, p) >> (lane & 31)) & 1u) << 31 : 0u;
+        if (lane < 32) {
+#pragma unroll
+          for (int p = 0; p < kPs; p += 4)
+            *reinterpret_cast<uint4*>(cons + lane * kPs + p) = make_uint4(ev[p], ev[p + 1], ev[p + 2], ev[p + 3]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      const unsigned* yn = ywp + 64 * (j + 1);
+      const unsigned nlo0 = yn[0], nlo1 = yn[1];
+      auto seg = [&](auto mask_t) {
+        constexpr bool MASK = decltype(mask_t)::value;
+        unsigned dq[4][2];
+#pragma unroll 4
+        for (int r = 0; r < 32; ++r) {
+          const int s = 32 * j + r;
+          const unsigned sh = 31u - (unsigned)r;
+          const unsigned y0 = __builtin_amdgcn_alignbit(hi0, lo0, sh);
+          const unsigned y1 = __builtin_amdgcn_alignbit(hi1, lo1, sh);
+          const uint32_t match = ~((x0 ^ y0) | (x1 ^ y1));
+          unsigned inj[kPs];
+#pragma unroll
+          for (int p = 0; p < kPs; p += 4) {
+            const uint4 c4 = *reinterpret_cast<const uint4*>(cons + r * kPs + p);
+            inj[p] = c4.x;
+            inj[p + 1] = c4.y;
+            inj[p + 2] = c4.z;
+            inj[p + 3] = c4.w;
+          }
+          uint32_t U[NV], fU[NQ1];
+#pragma unroll
+          for (int p = 0; p < NV; ++p) {
+            const unsigned T = (unsigned)__builtin_amdgcn_update_dpp((int)inj[p], (int)h[p], 0x138, 0xf, 0xf, false);
+            U[p] = __builtin_amdgcn_alignbit(h[p], T, 31);
+          }
+          if constexpr (C::NQ > 0) {
+#pragma unroll
+            for (int p = 0; p < NQ1; ++p) {
+              const unsigned T =
+                  (unsigned)__builtin_amdgcn_update_dpp((int)inj[NV + p], (int)f[p], 0x138, 0xf, 0xf, false);
+              fU[p] = __builtin_amdgcn_alignbit(f[p], T, 31);
+            }
+          } else {
+            fU[0] = 0u;
+          }
+          uint32_t D, Fs, Ee, Fe, vn[NV], en[NQ1];
+          step<C>(match, v, e, U, fU, vn, en, h, f, D, Fs, Ee, Fe);
+#pragma unroll
+          for (int p = 0; p < NV; ++p) v[p] = vn[p];
+#pragma unroll
+          for (int q = 0; q < NQ1; ++q) e[q] = en[q];
+          if constexpr (MASK) {  // columns <= 0 keep the left border
+            const int lim = s - 32 * lane;
+            const uint32_t M = lim <= 0 ? ~0u : (lim >= 32 ? 0u : ~((1u << lim) - 1u));
+#pragma unroll
+            for (int p = 0; p < NV; ++p) v[p] = (v[p] & ~M) | ((p < GO ? ~row1 : 0u) & M);
+            if constexpr (C::NQ > 0) {
+#pragma unroll
+              for (int q = 0; q < NQ1; ++q) e[q] |= M;
+            }
+          }
+          if (to_below && lane == 63) {  // the band's last row at column s - 2047
+            unsigned ow[kPs];
+#pragma unroll
+            for (int p = 0; p < kPs; ++p) ow[p] = p < NV ? h[p] : (p < kPl ? f[p - NV] : 0u);
+            unsigned* en_ = ring + ((s - 2047) & 63) * kPs;
+#pragma unroll
+            for (int p = 0; p < kPs; p += 4)
+              *reinterpret_cast<uint4*>(en_ + p) = make_uint4(ow[p], ow[p + 1], ow[p + 2], ow[p + 3]);
+          }
+          // four words per lane and step; every 2 steps one 8-byte store per
+          // word, 512 B contiguous across the wave
+          dq[0][r & 1] = D;
+          dq[1][r & 1] = Fs;
+          dq[2][r & 1] = Ee;
+          dq[3][r & 1] = Fe;
+          if ((r & 1) == 1) {
+            const int rel = (s >> 2) - blo;
+            if ((unsigned)rel < (unsigned)nblk) {
+              typedef unsigned u2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+              for (int w4 = 0; w4 < 4; ++w4)
+                __builtin_nontemporal_store(u2{dq[w4][0], dq[w4][1]},
+                                            reinterpret_cast<u2*>(mb + (int64_t)rel * 1024 + w4 * 256 + (s & 2) * 64));
+            }
+          }
+        }
+      };
+      if (j < 65) seg(std::true_type{});
+      else seg(std::false_type{});
+      hi0 = lo0;
+      hi1 = lo1;
+      lo0 = nlo0;
+      lo1 = nlo1;
+      // --- publish chunk k = j - 64 (columns 32 k .. + 31, complete after this segment)
+      const int k = j - 64;
+      if (to_below && k >= 0 && k <= kmax) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        unsigned word = 0;
+#pragma unroll
+        for (int p = 0; p < kPl; ++p) {
+          const unsigned bit = lane < 32 ? ring[((32 * k + lane) & 63) * kPs + p] >> 31 : 0u;
+          const unsigned wd = (unsigned)__ballot(bit != 0u);
+          word = lane == p ? wd : word;
+        }
+        if (gl) __hip_atomic_store((gu64*)(gout + (int64_t)k * kPs + lane), ((u64)a.epoch << 32) | word, BITS_RLX);
+      }
+    }
+    if (!ok) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add((gu32*)(a.done + pd.slot), 1u, BITS_RLX);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev + 1u == (unsigned)pd.nbands) {  // the pair's last band: every band has released
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // the walk is one latency-bound wave: let it issue ahead of the SIMD's fill waves
+      __builtin_amdgcn_s_setprio(3);
+      if (!a.dbg_notrace) {
+        trace_gotoh(a, pd, lane);
+      } else if (lane == 0) {
+        a.oplen[pd.slot] = 0;
+        a.endij[pd.slot] = make_int2(pd.m, pd.n);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+}
+
+template <int PXY, int GO, int GE>
+hipError_t gotoh_launch(const FillArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((nw_align_gotoh<PXY, GO, GE>), dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int PXY, int GO, int GE>
+int gotoh_occ() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&nw_align_gotoh<PXY, GO, GE>), 256,
+                                                   0) != hipSuccess)
+    return 1;
+  return n > 0 ? n : 1;
+}
+
+struct GotohEntry {
+  int pxy, go, ge;
+  hipError_t (*launch)(const FillArgs&, int, hipStream_t);
+  int (*occ)();
+};
+
+// The scorings instantiated (pxy, go, ge): C5's (3, 3, 1); the reference's
+// linear 3/2 and 5/1 as their degenerate affine case (go = 0, ge = pgap); and
+// the affine scorings of the GPU tests.  Others run on nw_align_pka /
+// nw_align_affine.
+#define NWK_GOTOH_ENTRY(p, o, e) {p, o, e, gotoh_launch<p, o, e>, gotoh_occ<p, o, e>},
+const GotohEntry kGotohSet[] = {
+    NWK_GOTOH_ENTRY(3, 3, 1)
+    NWK_GOTOH_ENTRY(3, 0, 2) NWK_GOTOH_ENTRY(5, 0, 1) NWK_GOTOH_ENTRY(3, 0, 1)
+    NWK_GOTOH_ENTRY(3, 4, 1) NWK_GOTOH_ENTRY(1, 2, 2) NWK_GOTOH_ENTRY(2, 1, 1) NWK_GOTOH_ENTRY(4, 2, 2)
+    NWK_GOTOH_ENTRY(4, 2, 1) NWK_GOTOH_ENTRY(2, 4, 2) NWK_GOTOH_ENTRY(3, 5, 2) NWK_GOTOH_ENTRY(9, 3, 2)
+};
+#undef NWK_GOTOH_ENTRY
+
+const GotohEntry* gotoh_find(int pxy, int go, int ge) {
+  for (const auto& g : kGotohSet)
+    if (g.pxy == pxy && g.go == go && g.ge == ge) return &g;
+  return nullptr;
+}
+
+}  // namespace
+
+bool gotoh_admissible(int pxy, int go, int ge, int alpha) { return alpha <= 4 && gotoh_find(pxy, go, ge) != nullptr; }
+
+int gotoh_granules(int go, int ge) { return (2 * (go + ge) + go + 3) & ~3; }
+
+hipError_t launch_gotoh(const FillArgs& a, int pxy, int go, int ge, int grid, hipStream_t s) {
+  const GotohEntry* g = gotoh_find(pxy, go, ge);
+  return g ? g->launch(a, grid, s) : hipErrorInvalidValue;
+}
+
+int gotoh_blocks_per_cu(int pxy, int go, int ge) {
+  const GotohEntry* g = gotoh_find(pxy, go, ge);
+  return g ? g->occ() : 1;
+}
+
+}  // namespace nwk

@@ -1,6 +1,7 @@
-// gotoh_bits.h -- bit-sliced Gotoh step (probe for a future nw_align_* affine
-// kernel; not part of libnwk).  One call evaluates 32 cells, one per bit, of
-// the affine recurrence (oracle/nw_oracle.c nwo_pair_affine):
+// nwk_gotoh_planes.h -- the bit-sliced Gotoh step of nw_align_gotoh
+// (nwk_gotoh.hip; also compiled on the host by tools/probe/gotoh_sim.cpp, whose
+// test pins the algebra cell by cell).  One call evaluates 32 cells, one per
+// bit, of the affine recurrence (oracle/nw_oracle.c nwo_pair_affine):
 //   E = min(E_left + ge, H_left + go + ge),  F = min(F_up + ge, H_up + go + ge),
 //   H = min(H_diag + (match ? 0 : pxy), E, F).
 //

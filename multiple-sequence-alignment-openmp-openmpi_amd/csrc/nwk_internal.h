@@ -29,8 +29,22 @@ enum Mode : int {
   kBits = 8,       // bit-sliced difference planes (nw_align_bits, nwk_bits.hip): 2048-row bands, 2-bit traceback
   kBitsStrip = 9,  // kBits as rolling strips (nw_align_strip): one wave per pair, every band in turn
   kCol = 10,       // bit-parallel columns (nw_align_col, nwk_col.hip): kBits' domain and storage, a pair's span n + ~96 x bands
+  kGotoh = 11,     // affine gaps as bit-sliced thermometer planes (nw_align_gotoh, nwk_gotoh.hip): 2048-row bands,
+                   // four traceback words per step (D, F-source, E-extend, F-extend), fused device walk
 };
 constexpr int kBitsRows = 2048;  // kBits: rows per band (64 lanes x 32 bits)
+
+// kGotoh geometry (nw_align_gotoh): lane t bit b holds row 32 t + b of a
+// 2048-row band, at (1-based) column s - 32 t - b at step s.  Storage: 4-step
+// blocks of 1024 dwords, word w (0 D, 1 F-source, 2 E-extend, 3 F-extend) of
+// step s, lane t at w * 256 + (s & 2) * 64 + 2 t + (s & 1).  Windowed
+// (bits_w > 0): band b keeps blocks gotoh_blk_lo(b) .. + bits_nblk, the steps
+// of its cells within bits_w columns of the diagonal j = i n / m.
+__host__ __device__ inline int gotoh_blk_lo(int b, int m, int n, int w) {
+  if (w <= 0) return 0;
+  const int64_t lo = (int64_t)b * kBitsRows * n / m - w;
+  return lo <= 0 ? 0 : (int)(lo >> 2);
+}
 
 // One pair of the batch.  All offsets are element offsets into the
 // batch-level arrays passed to the kernels.
@@ -208,6 +222,11 @@ int strip_blocks_per_cu(int pgap, int ring_dwords);
 // kCol (nwk_col.hip)
 hipError_t launch_col(const FillArgs& a, int pxy, int pgap, int grid, hipStream_t s);
 int col_blocks_per_cu(int pgap);
+// kGotoh (nwk_gotoh.hip): instantiated for a fixed set of (pxy, go, ge)
+bool gotoh_admissible(int pxy, int go, int ge, int alpha);
+int gotoh_granules(int go, int ge);  // granules per 32-column chunk of a band's last row
+hipError_t launch_gotoh(const FillArgs& a, int pxy, int go, int ge, int grid, hipStream_t s);
+int gotoh_blocks_per_cu(int pxy, int go, int ge);
 
 // Dwords of one band of the stored matrix.
 __host__ __device__ inline int64_t band_dwords(int bits, int sblocks) {

@@ -257,7 +257,7 @@ int nwk_ctx_create(const nwk_opts* opts, nwk_ctx** out) {
   if (const char* v = getenv("NWK_VERBOSE")) o.verbose = atoi(v);  // debug: diagnostics on stderr
   // option checks first: they need no device
   if (o.finalize < 0 || o.finalize > 3) return fail(NWK_EINVAL, "nwk_ctx_create: finalize must be 0..3");
-  if (o.kernel < 0 || o.kernel > 6) return fail(NWK_EINVAL, "nwk_ctx_create: kernel must be 0..6");
+  if (o.kernel < 0 || o.kernel > 7) return fail(NWK_EINVAL, "nwk_ctx_create: kernel must be 0..7");
   if (o.task_order < 0 || o.task_order > 2) return fail(NWK_EINVAL, "nwk_ctx_create: task_order must be 0..2");
   if (o.bits != 0 && o.bits != 4 && o.bits != 8 && o.bits != 16 && o.bits != 32)
     return fail(NWK_EINVAL, "nwk_ctx_create: bits must be 0/4/8/16/32");
@@ -464,8 +464,15 @@ int choose_plan(const nwk_ctx* c, const Scoring& sc, Plan* pl) {
     static const int affpk_env = getenv("NWK_AFFPK") ? atoi(getenv("NWK_AFFPK")) : 1;
     const bool pk = c->opts.kernel != 1 && affpk_env != 0 && c->alpha <= 4 && pka_admissible(sc);
     pl->mode = pk ? kAffinePk : kAffine;
+    // bit-sliced planes (nw_align_gotoh) where an instantiation exists for the
+    // scoring (C5's 3/3/1, the linear 3/2 and 5/1 as go = 0, the tests') and the
+    // alphabet fits two code planes; opts.kernel 7 asks for it, 1 keeps
+    // nw_align_affine, 2 / 3 nw_align_pka; NWK_GOTOH=0 disables it under "auto"
+    static const int gotoh_env = getenv("NWK_GOTOH") ? atoi(getenv("NWK_GOTOH")) : 1;
+    const bool want_gotoh = c->opts.kernel == 7 || (c->opts.kernel == 0 && gotoh_env != 0);
+    if (want_gotoh && gotoh_admissible(sc.pxy, sc.go, sc.ge, c->alpha)) pl->mode = kGotoh;
     pl->bits = 4;          // 4-bit traceback codes
-    pl->kind = pk ? 0 : 1;  // profile codes / raw bytes (compare)
+    pl->kind = pk || pl->mode == kGotoh ? 0 : 1;  // profile codes / raw bytes (compare)
     pl->K0 = 0;
     pl->K1 = pxy;
     return NWK_OK;
@@ -622,7 +629,7 @@ int64_t pka_nsb_of(int m, int n, int w) {
 // batches x budget overflowed int64 for large budgets.)
 template <class Need>
 int choose_window(int mode, int batches, int64_t budget, Need&& need) {
-  if (mode == kAffinePk && batches <= 0) return 8192;
+  if ((mode == kAffinePk || mode == kGotoh) && batches <= 0) return 8192;
   const int64_t nb = batches > 0 ? batches : 1;
   static const int cand[] = {8192, 6144, 4096, 3072, 2560, 2048, 1536, 1024};
   for (int wc : cand)
@@ -630,7 +637,27 @@ int choose_window(int mode, int batches, int64_t budget, Need&& need) {
   return 1024;
 }
 
-void footprint(PairWork* w, int bits, int mode, bool affine) {
+// kGotoh stored 4-step blocks per band: every block of the band's steps
+// 0 .. 32 (n / 32 + 65) - 1, or (bits_w > 0) from gotoh_blk_lo(b) on, the
+// steps j + r of its cells (R0 + 1 + r, j), |j - i n / m| <= w, r < 2048
+int64_t gotoh_nblk_of(int m, int n, int w) {
+  const int64_t all = 8 * ((int64_t)(n >> 5) + 65);
+  if (w <= 0) return all;
+  return std::min(all, ceil_div(2 * (int64_t)w + ceil_div((int64_t)kBitsRows * n, m) + 2052, 4) + 1);
+}
+
+// gran: kGotoh granules per 32-column chunk of a band's last row (gotoh_granules)
+void footprint(PairWork* w, int bits, int mode, bool affine, int gran = 0) {
+  if (mode == kGotoh) {
+    const int64_t nb = ceil_div(w->m, kBitsRows), nw = (w->n >> 5) + 1;
+    w->segops_b = w->segctl_b = 0;
+    w->spec = 0;
+    w->bits_nblk = (int)gotoh_nblk_of(w->m, w->n, w->bits_w);
+    w->mat_dw = nb * w->bits_nblk * 1024;
+    w->bnd_gr = (nb - 1) * nw * gran;
+    w->ops_b = round_up((int64_t)w->m + w->n, 256);  // (the walk writes whole 256-byte blocks)
+    return;
+  }
   if (mode == kBitsStrip) {
     w->segops_b = w->segctl_b = 0;
     w->spec = 0;
@@ -1134,6 +1161,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     if (col) pl.mode = kCol;
   }
   const bool bitsy = pl.mode == kBits || pl.mode == kBitsStrip || pl.mode == kCol;
+  const bool gotoh = pl.mode == kGotoh;
+  const int ggran = gotoh ? gotoh_granules(sc.go, sc.ge) : 0;
   st.bits = bitsy ? 2 : pl.bits;
   st.mode = pl.mode;
   int rc;
@@ -1157,13 +1186,13 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       if (chain) chain->ready[w.out] = 1;
       mark_ready(c, w.out);
     } else {
-      footprint(&w, pl.bits, pl.mode, sc.affine);
+      footprint(&w, pl.bits, pl.mode, sc.affine, ggran);
       dp.push_back(w);
     }
   }
   if (!dp.empty()) {
     if ((rc = build_encoding(c, pl.kind)) != NWK_OK) return rc;
-    if (bitsy && (rc = build_yw(c)) != NWK_OK) return rc;
+    if ((bitsy || gotoh) && (rc = build_yw(c)) != NWK_OK) return rc;
     if ((pl.mode == kPacked || band_pairs(pl.mode)) &&
         (rc = build_sel(c, pl.K0 < 0 ? 1 : 0, band_pairs(pl.mode) ? 64 : 1)) != NWK_OK)
       return rc;
@@ -1185,7 +1214,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   // more batches (C5: 4 of ~124 pairs, ~12 rounds of wave slots each).
   static const int win_env = getenv("NWK_BITS_WIN") ? atoi(getenv("NWK_BITS_WIN")) : -1;
   static const int winb_env = getenv("NWK_WIN_BATCHES") ? atoi(getenv("NWK_WIN_BATCHES")) : 0;
-  if ((bitsy || pl.mode == kAffinePk) && !dp.empty() && win_env != 0) {
+  if ((bitsy || pl.mode == kAffinePk || gotoh) && !dp.empty() && win_env != 0) {
     auto total_b = [&]() {
       int64_t mat = 0, bnd = 0, ops = 0;
       int64_t seg = 0;
@@ -1195,7 +1224,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     auto set_w = [&](int W) {
       for (auto& w : dp) {
         w.bits_w = W;
-        footprint(&w, pl.bits, pl.mode, sc.affine);
+        footprint(&w, pl.bits, pl.mode, sc.affine, ggran);
       }
     };
     int W = win_env > 0 ? win_env : 0;
@@ -1247,7 +1276,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         int wc = col_win_env > 0 ? col_win_env : (int)round_up(std::max<int64_t>(1024, (int64_t)(2.5 * est)), 256);
         if (W > 0) wc = std::min(wc, W);
         w.bits_w = wc;
-        footprint(&w, pl.bits, pl.mode, sc.affine);
+        footprint(&w, pl.bits, pl.mode, sc.affine, ggran);
       }
     }
   }
@@ -1299,8 +1328,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   // (profiles/r01/ab_affine_bpc.json)
   if (pl.mode == kAffine) bpc = std::min(bpc, 2);
   if (pl.mode == kAffinePk) bpc = std::min(bpc, 2);
+  if (gotoh) bpc = gotoh_blocks_per_cu(sc.pxy, sc.go, sc.ge);
   static const int bpc_cap = getenv("NWK_BPC") ? atoi(getenv("NWK_BPC")) : 0;
-  if (bpc_cap > 0) bpc = std::min(bpc_cap, bitsy ? bpc : fill_blocks_per_cu(pl.mode, pl.bits));
+  if (bpc_cap > 0) bpc = std::min(bpc_cap, bitsy || gotoh ? bpc : fill_blocks_per_cu(pl.mode, pl.bits));
   const int grid = bpc * c->cus;
   float ms = 0;
 
@@ -1421,7 +1451,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       PairDesc& d = pd[q];
       d.x_off = c->c_off[w.i];
       d.y_off = c->c_off[w.j];
-      d.e_off = bitsy ? c->yw_off[w.j] : c->e_off[w.j];
+      d.e_off = bitsy || gotoh ? c->yw_off[w.j] : c->e_off[w.j];
       d.xw_off = pl.mode == kBitsStrip ? c->yw_off[w.i] : 0;
       d.bits_np = pl.mode == kBitsStrip ? strip_np(w.n) : 0;
       d.prio = 0;
@@ -1430,8 +1460,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       d.ops_off = ops_base_b + oo;
       d.m = w.m;
       d.n = w.n;
-      d.nbands = (int)ceil_div(w.m, bitsy ? kBitsRows : kBandRows);
-      d.nchunks = pl.mode == kBitsStrip ? d.bits_np / 64 : (int)ceil_div(w.n, 64);
+      d.nbands = (int)ceil_div(w.m, bitsy || gotoh ? kBitsRows : kBandRows);
+      d.nchunks = pl.mode == kBitsStrip ? d.bits_np / 64 : gotoh ? (w.n >> 5) + 1 : (int)ceil_div(w.n, 64);
       d.sblocks = pl.mode == kBits        ? bits_sblocks(d.nchunks)
                   : pl.mode == kCol       ? col_sblocks(d.nchunks)
                   : pl.mode == kBitsStrip ? strip_sblocks(w.m, w.n)
@@ -1498,7 +1528,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     static const int order_env = getenv("NWK_ORDER") ? atoi(getenv("NWK_ORDER")) : -1;
     int order = order_env;
     if (order < 0 && pl.mode == kBits && c->opts.task_order > 0) order = c->opts.task_order == 1 ? 0 : 1;
-    if (order < 0) order = (pl.mode == kBits || pl.mode == kAffinePk) && ntasks > 4 * (int64_t)grid ? 1 : 0;
+    if (order < 0) order = (pl.mode == kBits || pl.mode == kAffinePk || gotoh) && ntasks > 4 * (int64_t)grid ? 1 : 0;
     if (pl.mode == kBitsStrip) order = 0;  // one task per pair, largest first
     // kCol: bands trail each other by ~96 steps, so a pair's bands dequeued
     // together run as one short pipeline: pair-major unless NWK_ORDER says otherwise
@@ -1592,7 +1622,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.dbg_notrace = (getenv("NWK_AFF_NOTRACE") || getenv("NWK_NOTRACE")) ? 1 : 0;
     fa.lin_mode = 0;
     fa.prog = nullptr;
-    fa.yw = bitsy ? c->d_yw.as<unsigned>() : nullptr;
+    fa.yw = bitsy || gotoh ? c->d_yw.as<unsigned>() : nullptr;
     fa.strip_ring = strip_ring;
     fa.retry = c->d_retry.as<int>();
     if (getenv("NWK_WATCHDOG")) {
@@ -1705,6 +1735,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       HIP_TRY(launch_col(fa, sc.pxy, sc.pgap, (int)std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     else if (pl.mode == kBitsStrip)
       HIP_TRY(launch_strip(fa, sc.pxy, sc.pgap, (int)std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
+    else if (gotoh)
+      HIP_TRY(launch_gotoh(fa, sc.pxy, sc.go, sc.ge, (int)std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     else
       HIP_TRY(launch_fill(pl.mode, pl.bits, fa, std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
@@ -2011,18 +2043,18 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         PairWork w = dp[pos + q];
         const int old_w = w.bits_w;
         w.bits_w = 0;
-        footprint(&w, pl.bits, pl.mode, sc.affine);
+        footprint(&w, pl.bits, pl.mode, sc.affine, ggran);
         auto need = [](const PairWork& x) {
           return x.mat_dw * 4 + x.bnd_gr * 8 + 3 * x.ops_b + x.segops_b + x.segctl_b + 8192;
         };
-        if (pl.mode == kAffinePk && need(w) > c->budget) {
+        if ((pl.mode == kAffinePk || gotoh) && need(w) > c->budget) {
           // the affine path has no linear-space fallback: re-run with the
           // widest doubled window that fits the budget instead of in full
           int nw = 0;
           for (int64_t cw = 2 * (int64_t)old_w; cw < (1 << 30); cw *= 2) {
             PairWork t = w;
             t.bits_w = (int)cw;
-            footprint(&t, pl.bits, pl.mode, sc.affine);
+            footprint(&t, pl.bits, pl.mode, sc.affine, ggran);
             if (need(t) > c->budget) break;
             nw = (int)cw;
             if (t.mat_dw >= w.mat_dw) break;  // as wide as full storage
@@ -2032,7 +2064,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
                         "neither full storage (%lld B) nor a %d-column window fits the HBM budget %lld",
                         (long long)w.id, w.m, w.n, old_w, (long long)need(w), 2 * old_w, (long long)c->budget);
           w.bits_w = nw;
-          footprint(&w, pl.bits, pl.mode, sc.affine);
+          footprint(&w, pl.bits, pl.mode, sc.affine, ggran);
         }
         if (dp.size() == dp.capacity())  // the async finalize holds pointers into dp
           return fail(NWK_ENOMEM, "pair %lld: too many window re-runs", (long long)w.id);

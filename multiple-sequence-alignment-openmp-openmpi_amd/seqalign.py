@@ -25,10 +25,11 @@ LIB_PATH = os.environ.get("NWK_LIB") or os.path.join(HERE, "lib", "libnwk.so")
 NWK_OK = 0
 ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "EKERNEL", -5: "ECOMM"}
 MODES = {0: "profile", 1: "compare", 2: "literal", 3: "affine", 4: "packed-profile", 5: "packed-band-pairs",
-         7: "packed-affine-band-pairs", 8: "bit-sliced-planes", 9: "bit-sliced-strips", 10: "bit-parallel-columns"}
+         7: "packed-affine-band-pairs", 8: "bit-sliced-planes", 9: "bit-sliced-strips", 10: "bit-parallel-columns",
+         11: "bit-sliced-affine"}
 # fill kernel of each mode (csrc/nwk_kernels.hip), as rocprofv3 names it
 KERNELS = {0: "nw_align", 1: "nw_align", 2: "nw_align", 3: "nw_align_affine", 4: "nw_align_pk", 5: "nw_align_pk2",
-           7: "nw_align_pka", 8: "nw_align_bits", 9: "nw_align_strip", 10: "nw_align_col"}
+           7: "nw_align_pka", 8: "nw_align_bits", 9: "nw_align_strip", 10: "nw_align_col", 11: "nw_align_gotoh"}
 
 
 class NwkError(RuntimeError):
@@ -108,6 +109,8 @@ KERNEL_SOURCES = {
                        "Makefile"),
     "nw_align_col": ("csrc/nwk_col.hip", "csrc/nwk_bits_dev.h", "csrc/nwk_sha_dev.h", "csrc/nwk_internal.h",
                      "Makefile"),
+    "nw_align_gotoh": ("csrc/nwk_gotoh.hip", "csrc/nwk_gotoh_planes.h", "csrc/nwk_bits_dev.h", "csrc/nwk_sha_dev.h",
+                       "csrc/nwk_internal.h", "Makefile"),
     "nw_align_pka": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
     "nw_align_pk2": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
     "nw_align_pk": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
@@ -194,7 +197,7 @@ class Engine:
     FINALIZE = {"auto": 0, "host": 1, "device": 2, "fused": 3}
 
     KERNEL = {"auto": 0, "nw_align": 1, "nw_align_pk": 2, "nw_align_pk2": 3, "nw_align_bits": 4, "nw_align_strip": 5,
-              "nw_align_col": 6}
+              "nw_align_col": 6, "nw_align_gotoh": 7}
 
     def __init__(self, device=0, bits=0, workspace_bytes=0, host_threads=0, verbose=False, finalize="auto",
                  linear_space=0, kernel="auto", task_order=0):

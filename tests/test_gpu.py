@@ -284,7 +284,8 @@ def test_affine_packed_windowed_storage_and_full_rerun(win):
     genes += _mutants(r, bytes(r.choice(ACGT) for _ in range(4500)), 2, ACGT)
     P, Q = (bytes(r.choice(ACGT) for _ in range(3000)) for _ in range(2))
     genes += [P + Q, Q + P]
-    env = dict(os.environ, **({} if win == "auto" else {"NWK_BITS_WIN": win}))
+    # (NWK_GOTOH=0: these scorings run on nw_align_gotoh by default, test_gpu_gotoh.py)
+    env = dict(os.environ, NWK_GOTOH="0", **({} if win == "auto" else {"NWK_BITS_WIN": win}))
     res = subprocess.run([sys.executable, "-c", _AFF_WIN_SCRIPT, os.path.dirname(seqalign.__file__), str(40 << 20)],
                          input=json.dumps([g.hex() for g in genes]).encode(), env=env,
                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
@@ -329,7 +330,7 @@ def test_affine_window_rerun_widens_when_full_storage_does_not_fit():
 
     import workloads
 
-    env = dict(os.environ, NWK_BITS_WIN="32")
+    env = dict(os.environ, NWK_BITS_WIN="32", NWK_GOTOH="0")
     res = subprocess.run([sys.executable, "-c", _AFF_WIDEN_SCRIPT, os.path.dirname(seqalign.__file__)],
                          env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
     assert res.returncode == 0, res.stderr.decode()[-2000:]
@@ -472,20 +473,28 @@ def test_affine_random_vs_oracle(engine, pxy, go, ge):
 
 
 # Packed affine fill (nw_align_pka, mode 7): ACGT-only sets with admissible
-# penalties run on it by default; every result must equal the oracle and the
-# unpacked nw_align_affine (opts.kernel = "nw_align" forces the latter).
+# penalties run on it by default where nw_align_gotoh has no instantiation
+# (opts.kernel = "nw_align_pk2" pins it); every result must equal the oracle
+# and the unpacked nw_align_affine (opts.kernel = "nw_align" forces the latter).
+
+
+@pytest.fixture(scope="module")
+def pka_engine():
+    e = seqalign.Engine(device=0, kernel="nw_align_pk2")
+    yield e
+    e.close()
 PKA_PARAMS = [(3, 3, 1), (1, 2, 2), (0, 5, 0), (7, 0, 3), (2, 1, 1), (5, 0, 0), (0, 0, 0), (9, 3, 2), (6, 6, 0)]
 PKA_LENS = [1, 2, 63, 64, 65, 511, 512, 513, 1023, 1024, 1025, 2100]
 
 
 @pytest.mark.parametrize("pxy,go,ge", PKA_PARAMS)
-def test_affine_packed_vs_oracle(engine, pxy, go, ge):
+def test_affine_packed_vs_oracle(pka_engine, pxy, go, ge):
     r = random.Random(7000 + pxy * 100 + go * 10 + ge)
     genes = [bytes(r.choice(ACGT) for _ in range(L)) for L in PKA_LENS]
     genes += _mutants(r, bytes(r.choice(ACGT) for _ in range(1500)), 3, ACGT)
-    engine.set_sequences(genes)
-    pen, hs = engine.align_pairs_affine(_all_ids(len(genes)), pxy, go, ge)
-    assert engine.stats()["mode"] == 7, "nw_align_pka expected"
+    pka_engine.set_sequences(genes)
+    pen, hs = pka_engine.align_pairs_affine(_all_ids(len(genes)), pxy, go, ge)
+    assert pka_engine.stats()["mode"] == 7, "nw_align_pka expected"
     h, opens, ohs = oracle.all_pairs_affine(genes, pxy, go, ge)
     assert [int(v) for v in pen] == opens
     assert [x.tobytes().hex() for x in hs] == ohs
@@ -493,28 +502,29 @@ def test_affine_packed_vs_oracle(engine, pxy, go, ge):
 
 @pytest.mark.parametrize("seed", range(3))
 def test_affine_packed_equals_unpacked(seed):
-    """Multi-band-pair pairs (3k-7k): nw_align_pka vs nw_align_affine, bit-exact."""
+    """Multi-band(-pair) pairs (3k-7k): nw_align_gotoh, nw_align_pka and
+    nw_align_affine, bit-exact against each other."""
     r = random.Random(8100 + seed)
     base = bytes(r.choice(ACGT) for _ in range(5000))
     genes = _rand_genes(r, 3, 3000, 7000, ACGT) + _mutants(r, base, 3, ACGT) + [b"A" * 4000, b"C" * 2500]
     pxy, go, ge = [(3, 3, 1), (4, 2, 1), (2, 4, 2)][seed]
     out = []
-    for kernel in ("auto", "nw_align"):
+    for kernel in ("nw_align_gotoh", "nw_align_pk2", "nw_align"):
         with seqalign.Engine(device=0, kernel=kernel) as e:
             e.set_sequences(genes)
             h, pen, hs = e.align_all(pxy, None, affine=(go, ge))
             out.append((e.stats()["mode"], h, [int(v) for v in pen], hs.tobytes()))
-    assert out[0][0] == 7 and out[1][0] == 3
-    assert out[0][1:] == out[1][1:]
+    assert [o[0] for o in out] == [11, 7, 3]
+    assert out[0][1:] == out[1][1:] == out[2][1:]
 
 
-def test_affine_packed_big13_degenerate(engine, golden):
+def test_affine_packed_big13_degenerate(pka_engine, golden):
     """big13 at full size on nw_align_pka with go=0, ge=pgap: the reference's published answer."""
     c = golden["big13"]
     pxy, pgap, genes = case_input(c)
-    engine.set_sequences(genes)
-    pen, hs = engine.align_pairs_affine(_all_ids(len(genes)), pxy, 0, pgap)
-    assert engine.stats()["mode"] == 7
+    pka_engine.set_sequences(genes)
+    pen, hs = pka_engine.align_pairs_affine(_all_ids(len(genes)), pxy, 0, pgap)
+    assert pka_engine.stats()["mode"] == 7
     assert [int(v) for v in pen] == c["penalties"]
     assert seqalign.chain_hash(hs) == c["hash"]
 
@@ -543,9 +553,10 @@ def test_affine_single_pair_strings(engine, m, n):
         assert engine.get_minimum_penalty_affine(x, y, pxy, go, ge) == oracle.pair_affine(x, y, pxy, go, ge)
 
 
-@pytest.mark.parametrize("kernel,mode", [("auto", 7), ("nw_align", 3)])
+@pytest.mark.parametrize("kernel,mode", [("auto", 11), ("nw_align_pk2", 7), ("nw_align", 3)])
 def test_affine_multi_batch_and_api(golden, kernel, mode):
-    """Multi-batch workspaces on nw_align_pka (default for ACGT) and nw_align_affine."""
+    """Multi-batch workspaces on nw_align_gotoh (default for ACGT and 3/4/1),
+    nw_align_pka and nw_align_affine."""
     r = random.Random(21)
     genes = _rand_genes(r, 7, 600, 1300, ACGT)
     with seqalign.Engine(device=0, workspace_bytes=3 << 20, kernel=kernel) as e:

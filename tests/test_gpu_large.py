@@ -124,7 +124,7 @@ def test_affine_window_choice_at_a_large_budget():
         e.set_sequences(genes)
         pa, _ = e.align_pairs_affine(np.arange(28, dtype=np.int64), 3, 3, 1)
         st = e.stats()
-    assert st["mode"] == 7 and st["window"] == 8192, st
+    assert st["mode"] in (7, 11) and st["window"] == 8192, st  # nw_align_gotoh / nw_align_pka
     assert st["batches"] == 1 and st["window_retries"] == 0, st
     for p in (0, 1):
         i, j = seqalign.pair_ij(p)

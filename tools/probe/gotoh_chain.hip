@@ -35,7 +35,7 @@
 #include <type_traits>
 #include <vector>
 
-#include "gotoh_bits.h"
+#include "../../multiple-sequence-alignment-openmp-openmpi_amd/csrc/nwk_gotoh_planes.h"
 
 using namespace gotoh_bits;
 using C5 = Cfg<3, 1, 3>;

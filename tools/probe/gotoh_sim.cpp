@@ -14,7 +14,7 @@
 #include <string>
 #include <vector>
 
-#include "gotoh_bits.h"
+#include "../../multiple-sequence-alignment-openmp-openmpi_amd/csrc/nwk_gotoh_planes.h"
 
 using namespace gotoh_bits;
 
