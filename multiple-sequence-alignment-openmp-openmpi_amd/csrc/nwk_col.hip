@@ -902,6 +902,7 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
     if (lane == 0) __hip_atomic_store((gu32*)(sinfo + 4 * sb), a.epoch, BITS_RLX);
     return;
   }
+  if (a.dbg_badwalk == pd.slot + 1) bad = true;  // (tests: a failed walk must never reach the host as a result)
   if (bad && lane == 0) atomicOr(a.err, 16u);
   if (a.stamps && lane == 0) {
     u64* x = a.stamps + 8 * pd.slot;
@@ -927,7 +928,7 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
     if (out) a.retry[pd.slot] = 1;
     if (a.host_rec) {
       int* h = a.host_rec + 4 * pd.slot;
-      h[1] = out ? -1 : o_len;
+      h[1] = out ? -1 : bad ? -2 : o_len;  // -1: re-run wider, -2: failed (never finalized)
       h[2] = o_end.x;
       h[3] = o_end.y;
     }

@@ -57,6 +57,37 @@ struct GGeo {
 #define NWK_GOTOH_WPE 4
 #endif
 
+// Waits until lanes 0 .. kPl - 1 hold granules tagged `epoch` (v: their last
+// reads).  A chunk's granules are one store instruction of the producing wave,
+// so only the last plane's lane polls -- one atomic read (at the coherence
+// point) per try, backing off 0.1 -> 1.6 us -- and once it has arrived every
+// stale lane re-reads.  (Every lane re-reading per try made the polls ~30% of
+// the launch's WRITE_SIZE: an atomic read counts as a write.)  Bounded like
+// bits_wait: ~4 s of wall time, or another wave's failure.
+template <int kPl>
+__device__ __noinline__ u64 gran_wait(const u64* p, unsigned epoch, u64 v, unsigned* err) {
+  const int lane = threadIdx.x & 63;
+  const bool mine = lane < kPl;
+  const u64 t0 = __builtin_amdgcn_s_memrealtime();
+  int nap = 1;
+  for (;;) {
+    if (__all(!mine || (unsigned)(v >> 32) == epoch)) return v;
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)err, BITS_RLX)) != 0u) return 0;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 400000000ull) {
+      if (lane == 0) atomicOr(err, 1u);
+      return 0;
+    }
+    const unsigned sent = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), kPl - 1);
+    if (sent != epoch) {
+      for (int z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(4);
+      nap = nap < 16 ? 2 * nap : 16;
+      if (lane == kPl - 1) v = __hip_atomic_fetch_add((gu64*)p, bits_opaque_zero(), BITS_RLX);
+    } else if (mine && (unsigned)(v >> 32) != epoch) {
+      v = __hip_atomic_fetch_add((gu64*)p, bits_opaque_zero(), BITS_RLX);
+    }
+  }
+}
+
 // ---- traceback ---------------------------------------------------------------
 
 struct Walk {
@@ -256,7 +287,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
           w = lane < GO ? h0 : (lane < NV ? 0u : ~0u);
         } else if (j <= kmax) {
           if (!__all(!gl || (unsigned)(g >> 32) == a.epoch)) {
-            g = bits_wait(gin + (int64_t)j * kPs + lane, gl, a.epoch, g, a.err);
+            g = gran_wait<kPl>(gin + (int64_t)j * kPs + lane, a.epoch, g, a.err);
             if (!__all(!gl || (unsigned)(g >> 32) == a.epoch)) {
               ok = false;
               break;

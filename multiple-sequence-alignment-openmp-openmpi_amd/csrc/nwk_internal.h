@@ -147,6 +147,7 @@ struct FillArgs {
   int K0, K1;              // diag increments in G-space: match, mismatch (kAffine: K1 = pxy)
   int go, ge;              // kAffine: gap open / extend
   int dbg_notrace;         // debug: skip the affine traceback
+  int dbg_badwalk;         // debug (tests): slot + 1 whose nw_align_col walk reports itself failed (err 16)
   int lin_mode;            // nw_align: 0 normal, 1 linear-space fill pass, 2 linear-space group recompute + trace
   unsigned* prog;          // debug: per-wave progress markers (NWK_WATCHDOG)
   unsigned* tdone;         // kPacked2: per task, 1 = filled and released
@@ -183,7 +184,7 @@ struct FillArgs {
   unsigned* fin_flag;      // per slot (host-mapped): = epoch once the record is written
   // Streamed host finalize (kCol, host-side finalize): the pair walk writes
   // its moves to host-mapped ops_host + (ops_off - ops_base) and then, per
-  // slot, host_rec {flag = epoch, length (-1: left the window), end i, end j}
+  // slot, host_rec {flag = epoch, length (-1: left the window, -2: the walk failed), end i, end j}
   // (flag last, system scope), so host threads finalize pairs during the launch.
   uint8_t* ops_host;
   int* host_rec;

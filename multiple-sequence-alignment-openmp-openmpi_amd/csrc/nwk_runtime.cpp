@@ -1161,8 +1161,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     if (col) pl.mode = kCol;
   }
   const bool bitsy = pl.mode == kBits || pl.mode == kBitsStrip || pl.mode == kCol;
-  const bool gotoh = pl.mode == kGotoh;
-  const int ggran = gotoh ? gotoh_granules(sc.go, sc.ge) : 0;
+  bool gotoh = pl.mode == kGotoh;
+  int ggran = gotoh ? gotoh_granules(sc.go, sc.ge) : 0;
   st.bits = bitsy ? 2 : pl.bits;
   st.mode = pl.mode;
   int rc;
@@ -1188,6 +1188,28 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     } else {
       footprint(&w, pl.bits, pl.mode, sc.affine, ggran);
       dp.push_back(w);
+    }
+  }
+  // nw_align_gotoh stores whole 2048-row bands plus their 2080-step skew, so a
+  // short pair costs more than on the band-pair kernels: a pair that does not
+  // fit the budget even at its 8192-column window runs the job on nw_align_pka
+  // (or nw_align_affine) instead.
+  if (gotoh) {
+    bool fits = true;
+    for (const auto& w : dp) {
+      PairWork t = w;
+      t.bits_w = 8192;
+      footprint(&t, pl.bits, pl.mode, sc.affine, ggran);
+      fits = fits && t.mat_dw * 4 + t.bnd_gr * 8 + 3 * t.ops_b + 8192 <= c->budget;
+    }
+    if (!fits) {
+      const bool pk = c->alpha <= 4 && pka_admissible(sc);
+      pl.mode = pk ? kAffinePk : kAffine;
+      pl.kind = pk ? 0 : 1;
+      st.mode = pl.mode;
+      gotoh = false;
+      ggran = 0;
+      for (auto& w : dp) footprint(&w, pl.bits, pl.mode, sc.affine, ggran);
     }
   }
   if (!dp.empty()) {
@@ -1620,6 +1642,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.K1 = pl.K1;
     fa.go = sc.go;
     fa.dbg_notrace = (getenv("NWK_AFF_NOTRACE") || getenv("NWK_NOTRACE")) ? 1 : 0;
+    fa.dbg_badwalk = getenv("NWK_DBG_BADWALK") ? atoi(getenv("NWK_DBG_BADWALK")) : 0;
     fa.lin_mode = 0;
     fa.prog = nullptr;
     fa.yw = bitsy || gotoh ? c->d_yw.as<unsigned>() : nullptr;
@@ -1822,7 +1845,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       const uint8_t* hops = c->h_opsm[par].as<uint8_t>();
       const int64_t obase = ops_base_b;
       fin.start([c, np, dwf, pdh, fsync, ep, hrec, hops, obase, sc, penalties, hashes, chain]() {
-        // state per pair: 0 pending, 1 claimed, 2 finalized, 3 left the window (re-run)
+        // state per pair: 0 pending, 1 claimed, 2 finalized, 3 left the window (re-run), 4 the
+        // walk failed (length -2: the launch reports the error; the pair is never finalized,
+        // reported or chained)
         std::unique_ptr<std::atomic<int>[]> state(new std::atomic<int>[(size_t)np]);
         for (int64_t q = 0; q < np; ++q) state[q].store(0, std::memory_order_relaxed);
         std::atomic<int64_t> nleft{np};
@@ -1839,7 +1864,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
               any = true;
               const int len = hrec[4 * q + 1];
               if (len < 0) {
-                state[q].store(3, std::memory_order_release);
+                state[q].store(len == -1 ? 3 : 4, std::memory_order_release);
               } else {
                 const PairWork& w = dwf[q];
                 Finalized f;

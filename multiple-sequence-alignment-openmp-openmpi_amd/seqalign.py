@@ -19,7 +19,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# NWK_LIB: an A/B build variant of the library (tools/col_variant.sh); default the in-tree build
+# NWK_LIB: an A/B build variant of the library (profiles/r04/scripts/col_variant.sh); default the in-tree build
 LIB_PATH = os.environ.get("NWK_LIB") or os.path.join(HERE, "lib", "libnwk.so")
 
 NWK_OK = 0

@@ -559,11 +559,18 @@ def test_affine_multi_batch_and_api(golden, kernel, mode):
     nw_align_pka and nw_align_affine."""
     r = random.Random(21)
     genes = _rand_genes(r, 7, 600, 1300, ACGT)
-    with seqalign.Engine(device=0, workspace_bytes=3 << 20, kernel=kernel) as e:
+    with seqalign.Engine(device=0, workspace_bytes=(12 << 20) if mode == 11 else (3 << 20), kernel=kernel) as e:
         e.set_sequences(genes)
         pen, hs = e.align_pairs_affine(_all_ids(len(genes)), 3, 4, 1)
         st = e.stats()
         assert st["batches"] > 1 and st["mode"] == mode
+        if kernel == "auto":  # a budget below one pair's nw_align_gotoh storage: the job runs on nw_align_pka
+            e2 = seqalign.Engine(device=0, workspace_bytes=3 << 20)
+            e2.set_sequences(genes)
+            p2, h2 = e2.align_pairs_affine(_all_ids(len(genes)), 3, 4, 1)
+            assert e2.stats()["mode"] == 7 and [int(v) for v in p2] == [int(v) for v in pen]
+            assert [x.tobytes() for x in h2] == [x.tobytes() for x in hs]
+            e2.close()
     h, opens, ohs = oracle.all_pairs_affine(genes, 3, 4, 1)
     assert [int(v) for v in pen] == opens and [x.tobytes().hex() for x in hs] == ohs
     pens = [0] * len(opens)

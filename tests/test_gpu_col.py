@@ -213,3 +213,92 @@ def test_col_fused_finalize_streamed(order):
     assert [int(v) for v in pen] == opens and [int(v) for v in pe] == opens
     assert [x.tobytes().hex() for x in hs] == ohs
     assert (he == hs).all()
+
+
+_HSTREAM_SCRIPT = r"""
+import json, sys, time
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import seqalign
+genes = [bytes.fromhex(g) for g in json.loads(sys.stdin.read())]
+k = len(genes)
+ids = np.arange(k * (k - 1) // 2, dtype=np.int64)
+out = {}
+with seqalign.Engine(device=0, kernel="nw_align_col", finalize="host", workspace_bytes=int(sys.argv[2])) as e:
+    e.set_sequences(genes)
+    if sys.argv[3] == "bad":  # a failed walk: nothing of it may be reported
+        e.align_pairs_begin(ids, 3, 2)
+        ups = []
+        t0 = time.time()
+        while time.time() - t0 < 60:
+            try:
+                u, _, _ = e.align_pairs_poll(0)
+            except seqalign.NwkError as x:
+                ups.append(-x.code)
+                break
+            ups.append(u)
+            time.sleep(0.001)
+        try:
+            e.align_pairs_end()
+            out["end"] = "ok"
+        except seqalign.NwkError as x:
+            out["end"] = x.code
+        out["ups"] = sorted(set(ups))
+    else:
+        pen, hs = e.align_pairs(ids, 3, 2)
+        st = e.stats()
+        out["sync"] = {"pen": [int(v) for v in pen], "hs": [x.tobytes().hex() for x in hs],
+                       "retries": st["window_retries"], "batches": st["batches"], "mode": st["mode"]}
+        e.align_pairs_begin(ids, 3, 2)
+        got = 0
+        while got < len(ids):
+            got, _, _ = e.align_pairs_poll(0)
+            time.sleep(0.0005)
+        pen2, hs2 = e.align_pairs_end()
+        out["async"] = {"pen": [int(v) for v in pen2], "hs": [x.tobytes().hex() for x in hs2]}
+print(json.dumps(out))
+"""
+
+
+def _hstream_genes():
+    r = random.Random(4711)
+    base = bytes(r.choice(ACGT) for _ in range(6000))
+    genes = [base, _mutants(r, base, 1, ACGT)[0]]  # pair 0 (1, 0): the largest
+    genes += [bytes(r.choice(ACGT) for _ in range(L)) for L in (700, 2100, 3300, 4000)]
+    P, Q = (bytes(r.choice(ACGT) for _ in range(2400)) for _ in range(2))
+    genes += [P + Q, Q + P]  # paths ~2400 columns off the diagonal
+    return genes
+
+
+def _run_hstream(genes, mode, ws, **env):
+    res = subprocess.run([sys.executable, "-c", _HSTREAM_SCRIPT, os.path.dirname(seqalign.__file__), str(ws), mode],
+                         input=json.dumps([g.hex() for g in genes]).encode(), env=dict(os.environ, **env),
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
+    assert res.returncode == 0, res.stderr.decode()[-2000:]
+    return json.loads(res.stdout.decode().strip().splitlines()[-1])
+
+
+def test_col_streamed_host_finalize_window_reruns_and_poll():
+    """The streamed host finalize (nw_align_col with host finalize: the walk
+    writes its moves to host-mapped memory and flags each pair; host threads
+    finalize during the launch) under forced window re-runs (NWK_BITS_WIN=48)
+    and several batches, through align_pairs and align_pairs_begin / poll / end:
+    bit-exact vs the oracle both ways."""
+    genes = _hstream_genes()
+    out = _run_hstream(genes, "ok", 120 << 20, NWK_BITS_WIN="48")
+    _, opens, ohs = oracle.all_pairs(genes, 3, 2)
+    s = out["sync"]
+    assert s["mode"] == 10 and s["retries"] > 0 and s["batches"] >= 2, s
+    assert s["pen"] == opens and s["hs"] == ohs
+    assert out["async"]["pen"] == opens and out["async"]["hs"] == ohs
+
+
+def test_col_streamed_host_finalize_failed_walk_never_reported():
+    """A walk that fails (NWK_DBG_BADWALK=1 marks slot 0's walk -- pair 0, the
+    batch's largest -- as failed, as a walk running past m + n would be) is
+    published with length -2: the host never finalizes, reports or chains it,
+    so poll never gets past pair 0, and the call ends with NWK_EKERNEL."""
+    genes = _hstream_genes()
+    out = _run_hstream(genes, "bad", 8 << 30, NWK_DBG_BADWALK="1")
+    assert out["end"] == -4, out
+    assert all(u <= 0 or u == 4 for u in out["ups"]), out  # upto stayed 0 (or the poll raised EKERNEL)
