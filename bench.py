@@ -279,9 +279,10 @@ def spawn_ranks(n):
     port = s.getsockname()[1]
     s.close()
     procs = []
+    run_id = os.urandom(8).hex()  # names this launch's rendezvous files / shared memory (dist.run_key)
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NWK_RUN_ID=run_id)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     return wait_ranks(procs)
 
@@ -420,6 +421,16 @@ def main():
     # sharded linear runs: the shard in `chunks` pieces, each piece's records
     # all-gathered (and chained on rank 0) while the next piece aligns
     chunks = int(os.environ.get("NWK_BENCH_CHUNKS", "0")) or (16 if stream else nwdist_auto_chunks(P, world))
+    # streamed jobs with every rank on this node: the pieces' records reach rank
+    # 0's chain through shared memory as they stream out of each rank's launch,
+    # and the whole shard's records go through ONE RCCL all-gather after it (an
+    # RCCL kernel cannot start while the persistent fill holds every SIMD's
+    # registers: dist.NodeRecords).  NWK_NODE_RECORDS=0: one
+    # all-gather per piece instead.
+    node = None
+    if stream and nwdist.node_local(world) and os.environ.get("NWK_NODE_RECORDS", "1") != "0":
+        node = nwdist.NodeRecords(comm, chunks, nwdist.chunk_parts(lengths, rank, world, chunks)[1])
+    token = [0]
     piece_stats = []
     last_hs = [None]
     piece_t = []  # per piece: ms from the step's start until its records were ready on this rank
@@ -430,8 +441,9 @@ def main():
         hs = None
         t_step = time.perf_counter()
         if stream:
+            token[0] += 1
             h, pen, hs = nwdist.align_sharded_streamed(
-                eng, lengths, pxy, pgap, rank, world, chunks=chunks, comm=comm,
+                eng, lengths, pxy, pgap, rank, world, chunks=chunks, comm=comm, node=node, token=token[0],
                 on_piece=lambda c: piece_t.append(round((time.perf_counter() - t_step) * 1e3, 3)))
             piece_stats.append(eng.stats())  # (the call has ended inside)
         elif sharded and not affine:
@@ -480,6 +492,8 @@ def main():
         dt = comm.max(dt)  # the slowest rank's time
     if rank != 0:
         eng.close()
+        if node is not None:
+            node.close()
         comm.close()
         return
 
@@ -508,7 +522,10 @@ def main():
                  if st["mode"] == 7 else
                  "u32 bit planes (bit-sliced: 32 cells per VALU op, 2*pgap thermometer planes of the "
                  "G-space differences; int32-exact results, 2-bit traceback storage)"
-                 if st["mode"] in (8, 9, 10) else ("int32" if st["bits"] == 32 else
+                 if st["mode"] in (8, 9, 10) else
+                 "u32 bit planes (bit-sliced Gotoh: 32 cells per VALU op, 2(go+ge) difference and go gap-offset "
+                 "thermometer planes; int32-exact results, 4 traceback bits per cell)"
+                 if st["mode"] == 11 else ("int32" if st["bits"] == 32 else
                                               "int32 (%d-bit mod-2^W traceback storage)" % st["bits"]),
         "data": "reference input file (mseq-big13-example.txt)" if args.workload == "big13"
                 else "synthetic (seeded MT19937 ACGT, workloads.py)",
@@ -529,7 +546,10 @@ def main():
                              fill_ms / launches * 1e-3, my_cells, launches),
     }
     if sharded:
-        out["collective"] = {"backend": comm.backend, "all_gathers_per_step": 1 if affine else chunks,
+        out["collective"] = {"backend": comm.backend,
+                             "all_gathers_per_step": 1 if affine or node is not None else chunks,
+                             "piece_exchange": "node shared memory (dist.NodeRecords), then one all-gather"
+                                               if node is not None else "one all-gather per piece",
                              "record_bytes": 72, "forced_at_world_1": world == 1,
                              "pieces_per_rank": 1 if affine else chunks,
                              "piece_ready_ms": list(piece_t)}  # rank 0, last timed step
@@ -542,6 +562,8 @@ def main():
                                            expect_hs=last_hs[0] if ok_gpu else None)
     print(json.dumps(out), flush=True)
     eng.close()
+    if node is not None:
+        node.close()
     if comm is not None:
         comm.close()
     if answer_ok is False:

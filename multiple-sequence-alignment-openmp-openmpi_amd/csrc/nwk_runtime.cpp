@@ -270,7 +270,20 @@ int nwk_ctx_create(const nwk_opts* opts, nwk_ctx** out) {
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, c->device));
   c->cus = prop.multiProcessorCount;
-  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  // NWK_CU_RESERVE=r (experiment, tools/overlap_probe.py): the engine's stream
+  // runs on all but r CUs (a CU mask), and the persistent grids are sized for
+  // the rest, so a collective launched on another stream (RCCL's kernels need
+  // 248-256 VGPRs and 37.7 KB of LDS per 256-thread block) finds room while a
+  // fill launch holds every other CU's register file
+  const int reserve = getenv("NWK_CU_RESERVE") ? atoi(getenv("NWK_CU_RESERVE")) : 0;
+  if (reserve > 0 && reserve < c->cus) {
+    std::vector<uint32_t> mask((size_t)(c->cus + 31) / 32, 0u);
+    for (int q = 0; q < c->cus - reserve; ++q) mask[(size_t)q / 32] |= 1u << (q % 32);
+    HIP_TRY(hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)mask.size(), mask.data()));
+    c->cus -= reserve;
+  } else {
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  }
   for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
   size_t fr = 0, tot = 0;
   HIP_TRY(hipMemGetInfo(&fr, &tot));

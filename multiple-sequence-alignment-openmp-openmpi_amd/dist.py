@@ -18,6 +18,18 @@ some ranks hanging in the all-gather.
 Communicators: RcclComm (the GPU ranks: RCCL through the library's own
 nwk_comm_*, so a rank process maps one HIP runtime and one RCCL and never
 imports torch) or TorchComm (torch.distributed: gloo in the CPU tests).
+
+Streamed jobs on one node (align_sharded_streamed with a NodeRecords): an RCCL
+collective cannot run while a rank's persistent fill launch holds the GPU --
+the fill's 4 waves/SIMD x 128 VGPRs fill every SIMD's register file, and RCCL's
+kernel needs 248-256 VGPRs and 37.7 KB of LDS per block; measured, even a
+one-wave kernel waits ~8 ms until the launch drains, and reserving CUs does
+not free RCCL-shaped blocks (tools/overlap_probe*.py, profiles/r05/overlap).
+So the pieces' records travel to rank 0's chain through node-local shared
+memory as they stream out of each rank's launch (the way sub:305-331's master
+takes results as workers finish), and the records of the whole shard go
+through ONE RCCL all-gather after the launch -- the collective of record, whose
+result rank 0 checks against what the chain consumed.
 """
 import os
 import time
@@ -137,14 +149,48 @@ class RcclComm:
         self.comm.close()
 
 
+def process_start_time():
+    """Wall-clock start of this process (s since the epoch)."""
+    try:
+        import psutil
+
+        return psutil.Process().create_time()
+    except Exception:
+        return _IMPORT_TIME
+
+
+_IMPORT_TIME = time.time()
+
+
+def read_rendezvous_id(path, rank, not_before, timeout_s, poll_s=0.01, nbytes=None):
+    """The RCCL unique id rank 0 wrote to `path`: only a complete file written
+    after `not_before` (this rank's start) counts, so a file left by an earlier
+    run that died before removing it is never used (its ncclCommInitRank would
+    hang on a mismatched id)."""
+    nbytes = nbytes or seqalign.COMM_ID_BYTES
+    t0 = time.time()
+    while True:
+        try:
+            if os.path.getmtime(path) >= not_before - 1.0:
+                with open(path, "rb") as f:
+                    uid = f.read()
+                if len(uid) == nbytes:
+                    return uid
+        except OSError:
+            pass
+        if time.time() - t0 > timeout_s:
+            raise RuntimeError("rank %d: no RCCL id from rank 0 at %s after %.0f s" % (rank, path, timeout_s))
+        time.sleep(poll_s)
+
+
 def rccl_comm(device, world, rank, timeout_s=120.0):
     """RcclComm for this rank process.  Rendezvous on the node: rank 0 writes
-    the RCCL id to a file named by the launcher (the ranks' common parent
-    process) and MASTER_PORT; the other ranks wait for it.  All ranks of a
-    bench run are on one node (torch.distributed.run --nnodes=1, or bench.py's
-    own spawn)."""
-    key = "%s_%s" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
-    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "nwk_rccl_id_%s" % key)
+    the RCCL id to a file named by the launch (run_key: the launcher's run id,
+    else MASTER_PORT and the ranks' common parent); the other ranks wait for a
+    complete file written after they started (read_rendezvous_id).  All ranks
+    of a bench run are on one node (torch.distributed.run --nnodes=1, or
+    bench.py's own spawn)."""
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "nwk_rccl_id_%s" % run_key())
     if rank == 0:
         uid = seqalign.Comm.unique_id()
         tmp = path + ".tmp%d" % os.getpid()
@@ -152,18 +198,7 @@ def rccl_comm(device, world, rank, timeout_s=120.0):
             f.write(uid)
         os.replace(tmp, path)
     else:
-        t0 = time.time()
-        while True:
-            try:
-                with open(path, "rb") as f:
-                    uid = f.read()
-                if len(uid) == seqalign.COMM_ID_BYTES:
-                    break
-            except OSError:
-                pass
-            if time.time() - t0 > timeout_s:
-                raise RuntimeError("rank %d: no RCCL id from rank 0 at %s after %.0f s" % (rank, path, timeout_s))
-            time.sleep(0.01)
+        uid = read_rendezvous_id(path, rank, process_start_time(), timeout_s)
     comm = RcclComm(seqalign.Comm(device, uid, world, rank))
     comm.barrier()  # every rank has read the id
     if rank == 0:
@@ -333,6 +368,96 @@ class StreamedShard:
         return self.err
 
 
+class NodeRecords:
+    """Per-piece record blocks of every rank of one node, in POSIX shared
+    memory: rank r's block of piece c (per[c] records) at slot (r, c), then its
+    flag (int64) set to the step's token.  Stores are ordered by the x86-64
+    memory model (TSO, every MI355X host): a reader that sees the flag sees the
+    block.  Rank 0 creates the segment (a stale one of the same name is
+    replaced) and stamps it with a nonce that every rank receives through the
+    communicator before attaching, so no rank can read a segment left by an
+    earlier run."""
+
+    def __init__(self, comm, chunks, per, key=None):
+        from multiprocessing import shared_memory
+
+        self.world, self.rank, self.chunks = comm.world, comm.rank, chunks
+        self.per = [int(x) for x in per]
+        self.pre = np.cumsum([0] + self.per)
+        self.sum_per = int(self.pre[-1])
+        key = key or run_key()
+        self.name = "nwk_rec_%s" % key
+        flags_b = 8 * self.world * chunks
+        self.data_off = 64 + (flags_b + 63) // 64 * 64
+        size = self.data_off + self.world * self.sum_per * REC
+        nonce = 0
+        if self.rank == 0:
+            try:  # a segment left by a run that died
+                old = shared_memory.SharedMemory(name=self.name)
+                old.close()
+                old.unlink()
+            except FileNotFoundError:
+                pass
+            self.shm = shared_memory.SharedMemory(name=self.name, create=True, size=size)
+            nonce = int.from_bytes(os.urandom(6), "little") | 1
+            np.ndarray((1,), dtype=np.int64, buffer=self.shm.buf)[0] = nonce
+        nonce = int(comm.max(float(nonce)))  # rank 0's nonce (< 2^53), after it created the segment
+        if self.rank != 0:
+            self.shm = shared_memory.SharedMemory(name=self.name)
+            if int(np.ndarray((1,), dtype=np.int64, buffer=self.shm.buf)[0]) != nonce:
+                raise RuntimeError("rank %d: node record segment %s is not this run's" % (self.rank, self.name))
+        self.flags = np.ndarray((self.world, chunks), dtype=np.int64, buffer=self.shm.buf, offset=64)
+        self.data = np.ndarray((self.world, self.sum_per, REC), dtype=np.uint8, buffer=self.shm.buf,
+                               offset=self.data_off)
+        if self.rank == 0:
+            self.flags[:] = 0
+
+    def publish(self, c, block, token):
+        """This rank's padded block of piece c, then its flag."""
+        self.data[self.rank, self.pre[c]:self.pre[c + 1]] = block
+        self.flags[self.rank, c] = token
+
+    def wait(self, c, token, poll_s=20e-6, timeout_s=600.0):
+        """Every rank's block of piece c (rank-major, as an all-gather returns them)."""
+        t0 = time.time()
+        while not (self.flags[:, c] == token).all():
+            if time.time() - t0 > timeout_s:
+                raise RuntimeError("node records: piece %d not published by every rank in %.0f s" % (c, timeout_s))
+            time.sleep(poll_s)
+        return self.data[:, self.pre[c]:self.pre[c + 1]].reshape(-1, REC).copy()
+
+    def shard_blocks(self):
+        """Every rank's whole padded shard (rank-major), as this rank published it."""
+        return self.data.reshape(-1, REC)
+
+    def close(self):
+        shm, self.shm = getattr(self, "shm", None), None
+        if shm is None:
+            return
+        self.flags = self.data = None
+        shm.close()
+        if self.rank == 0:
+            try:
+                shm.unlink()
+            except FileNotFoundError:
+                pass
+
+
+def run_key():
+    """A name shared by the ranks of one launch: the launcher's run id
+    (TORCHELASTIC_RUN_ID; NWK_RUN_ID from bench.py's own spawn), else
+    MASTER_PORT and the ranks' common parent process."""
+    rid = os.environ.get("NWK_RUN_ID") or os.environ.get("TORCHELASTIC_RUN_ID")
+    if rid:
+        return "".join(ch for ch in rid if ch.isalnum())[:40] + "_%s" % os.environ.get("MASTER_PORT", "0")
+    return "%s_%s" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
+
+
+def node_local(world):
+    """All ranks of the job on this node (torchrun's LOCAL_WORLD_SIZE, or bench.py's own spawn)."""
+    return int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
+
+
 def any_rank_failed(failed, comm):
     """One status collective (all-reduce MAX of a flag): True on every rank
     when any rank failed."""
@@ -391,8 +516,52 @@ def align_sharded_pipelined(eng, lengths, pxy, pgap, rank, world, chunks=1, devi
     return _exchange(shard, chunks, rank, P, default_comm(comm, device, group), final_status=False)
 
 
+def _exchange_node(shard, chunks, rank, P, comm, node, token):
+    """The streamed pipeline with node-local piece exchange (NodeRecords):
+    every rank publishes each piece's block as its records are in, rank 0's
+    chain worker takes piece c once every rank has published it, and after the
+    launch the whole shard's records go through ONE all-gather (RCCL on the GPU
+    ranks) -- rank 0 checks that it returns exactly what the chain consumed.
+    Failure contract as _exchange: a failed rank publishes FAILED-tagged blocks
+    and joins both collectives; every rank raises."""
+    chain = seqalign.ChainStream(P) if rank == 0 else None
+    err = None
+    blocks = []
+    try:
+        shard.start()
+        for c in range(chunks):
+            b = shard.block(c)
+            blocks.append(b)
+            node.publish(c, b, token)
+            if chain is None or err is not None:
+                continue
+            try:
+                cid, cpen, chs = unpack_chunk(node.wait(c, token))
+            except RankFailed as e:
+                err = e
+                continue
+            chain.feed(cid, cpen, chs)
+        own = shard.finish()
+        err = own if own is not None else err
+        mine = np.concatenate(blocks) if own is None else failed_block(node.sum_per)
+        g = comm.all_gather(mine)  # the collective of record: every rank's whole shard
+        if any_rank_failed(err is not None, comm) and err is None:
+            err = RankFailed("a peer rank failed")
+        if err is not None:
+            raise RankFailed("rank %d: %s" % (rank, err)) from err
+        if chain is None:
+            return None, None, None
+        if not np.array_equal(np.asarray(g, dtype=np.uint8).reshape(-1, REC), node.shard_blocks()):
+            raise RuntimeError("rank 0: the all-gathered records differ from the node records the chain took")
+        return chain.finish()
+    finally:
+        shard.finish()
+        if chain is not None:
+            chain.close()
+
+
 def align_sharded_streamed(eng, lengths, pxy, pgap, rank, world, chunks=8, device=None, group=None,
-                           on_piece=None, poll_s=50e-6, comm=None):
+                           on_piece=None, poll_s=50e-6, comm=None, node=None, token=1):
     """The shard as ONE launch whose per-pair records stream to the host as
     pairs are hashed inside the fill launch (StreamedShard).  Piece c -- the
     shard's ids below the global threshold P (c+1) / chunks -- goes through its
@@ -401,11 +570,17 @@ def align_sharded_streamed(eng, lengths, pxy, pgap, rank, world, chunks=8, devic
     Same return value and failure contract as align_sharded_pipelined, plus one
     status collective after the launch has ended: a rank whose failure only the
     end of its call reports (after its records were already exchanged) makes
-    every rank, rank 0 included, raise instead of returning a hash."""
+    every rank, rank 0 included, raise instead of returning a hash.
+    node (a NodeRecords over the same chunks, all ranks on this node): the
+    pieces reach rank 0 through shared memory and ONE all-gather follows the
+    launch (_exchange_node); token: this call's flag value (the same on every
+    rank, different from the previous call's)."""
     k = len(lengths)
     P = k * (k - 1) // 2
     parts, per = chunk_parts(lengths, rank, world, chunks)
     shard = StreamedShard(eng, parts, per, pxy, pgap, poll_s=poll_s, on_piece=on_piece)
+    if node is not None:
+        return _exchange_node(shard, chunks, rank, P, default_comm(comm, device, group), node, token)
     return _exchange(shard, chunks, rank, P, default_comm(comm, device, group), final_status=True)
 
 

@@ -114,14 +114,17 @@ def test_bench_nccl_all_gather_at_world_one():
 
 
 @pytest.mark.gpu
-def test_two_ranks_streamed_records_big13_published_hash():
+@pytest.mark.parametrize("node", ["1", "0"])
+def test_two_ranks_streamed_records_big13_published_hash(node):
     """dist.align_sharded_streamed: one launch per rank (the engine's default
     task order: largest pairs first, so records arrive in size order, not in
-    canonical order), four pieces each exchanged once all of its records have
-    arrived, rank 0 chaining each piece; the line records when each piece was
+    canonical order), four pieces each handed to rank 0's chain once all of its
+    records have arrived -- through node shared memory and one all-gather of
+    the whole shards (node=1, dist.NodeRecords, the default on one node), or
+    one all-gather per piece (node=0); the line records when each piece was
     ready."""
     env = _env(NWK_BENCH_BACKEND="gloo", NWK_BENCH_SHARE_GPU="1", NWK_BENCH_WS_GB="110",
-                     NWK_BENCH_STREAM="1", NWK_BENCH_CHUNKS="4")
+               NWK_BENCH_STREAM="1", NWK_BENCH_CHUNKS="4", NWK_NODE_RECORDS=node)
     r = subprocess.run([sys.executable, "-u", BENCH, "--gpus", "2", "--workload", "big13",
                         "--steps", "1", "--warmup", "0", "--no-cpu-baseline"], stdout=subprocess.PIPE,
                        stderr=subprocess.PIPE, env=env, timeout=110)
@@ -131,3 +134,5 @@ def test_two_ranks_streamed_records_big13_published_hash():
     assert "streamed" in line["config"]["parallelism"]
     ready = line["collective"]["piece_ready_ms"]
     assert len(ready) == 4 and ready == sorted(ready)
+    assert line["collective"]["piece_exchange"].startswith("node" if node == "1" else "one all-gather per piece")
+    assert line["collective"]["all_gathers_per_step"] == (1 if node == "1" else 4)

@@ -7,6 +7,7 @@ for the CPU oracle (test infrastructure), since this container has no GPU.
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -264,7 +265,7 @@ class _OracleStreamEngine(_OracleEngine):
         return self._pen, self._hs
 
 
-def _streamed_worker(rank, world, port, cases, chunks, fail, q):
+def _streamed_worker(rank, world, port, cases, chunks, fail, q, node_records=False, steps=1):
     import sys
 
     for p in (PKG, ORACLE):
@@ -276,22 +277,34 @@ def _streamed_worker(rank, world, port, cases, chunks, fail, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         for name, pxy, pgap, genes in cases:
-            eng = _OracleStreamEngine(genes, fail_end=fail and rank == world - 1)
+            lens = [len(g) for g in genes]
+            node = None
+            if node_records:  # pieces through node shared memory, then ONE all-gather
+                node = nwdist.NodeRecords(nwdist.TorchComm(), chunks, nwdist.chunk_parts(lens, rank, world, chunks)[1])
             try:
-                h, pen, _ = nwdist.align_sharded_streamed(eng, [len(g) for g in genes], pxy, pgap, rank, world,
-                                                          chunks=chunks, poll_s=0.0)
-                q.put((rank, name, h, None if pen is None else [int(v) for v in pen]))
-            except nwdist.RankFailed as e:
-                q.put((rank, name, "raised: %s" % e, None))
+                for step in range(1, steps + 1):  # (the segment is reused across steps: token = step)
+                    eng = _OracleStreamEngine(genes, fail_end=fail and rank == world - 1)
+                    try:
+                        h, pen, _ = nwdist.align_sharded_streamed(eng, lens, pxy, pgap, rank, world, chunks=chunks,
+                                                                  poll_s=0.0, node=node, token=step)
+                        q.put((rank, name, h, None if pen is None else [int(v) for v in pen]))
+                    except nwdist.RankFailed as e:
+                        q.put((rank, name, "raised: %s" % e, None))
+            finally:
+                if node is not None:
+                    node.close()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 4)])
-def test_gloo_streamed_pieces_match_golden(world, chunks):
+@pytest.mark.parametrize("world,chunks,node", [(2, 1, False), (3, 4, False), (2, 1, True), (3, 4, True)])
+def test_gloo_streamed_pieces_match_golden(world, chunks, node):
     """dist.align_sharded_streamed (one launch per rank, records polled as they
-    stream, one all-gather per piece, final status collective): the answer
-    hash and penalties of the reference (golden) on rank 0."""
+    stream; one all-gather per piece, or -- node=True -- the pieces through
+    node shared memory (NodeRecords) and one all-gather of the whole shards,
+    checked against what the chain took; final status collective): the answer
+    hash and penalties of the reference (golden) on rank 0, over two steps that
+    reuse the node segment."""
     cases = []
     for c in CASES:
         pxy, pgap, genes = case_input(c)
@@ -299,11 +312,12 @@ def test_gloo_streamed_pieces_match_golden(world, chunks):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_streamed_worker, args=(r, world, port, cases, chunks, False, q))
+    steps = 2 if node else 1
+    procs = [ctx.Process(target=_streamed_worker, args=(r, world, port, cases, chunks, False, q, node, steps))
              for r in range(world)]
     for p in procs:
         p.start()
-    out = [q.get(timeout=300) for _ in range(world * len(cases))]
+    out = [q.get(timeout=300) for _ in range(world * len(cases) * steps)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -316,17 +330,19 @@ def test_gloo_streamed_pieces_match_golden(world, chunks):
             assert h is None
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_streamed_failure_at_end_raises_everywhere(world):
+@pytest.mark.parametrize("world,node", [(2, False), (3, False), (2, True), (3, True)])
+def test_gloo_streamed_failure_at_end_raises_everywhere(world, node):
     """The last rank's error surfaces only at align_pairs_end, after all of its
     records were exchanged and chained by rank 0: the final status collective
-    makes every rank -- rank 0 included -- raise instead of returning a hash."""
+    makes every rank -- rank 0 included -- raise instead of returning a hash
+    (also when the pieces went through node shared memory)."""
     genes = [b"ACGT" * 5, b"AC" * 7, b"GATTACA", b"T" * 11, b"CAT" * 4, b"GG" * 6, b"TACG" * 3]
     cases = [("f", 3, 2, genes)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_streamed_worker, args=(r, world, port, cases, 3, True, q)) for r in range(world)]
+    procs = [ctx.Process(target=_streamed_worker, args=(r, world, port, cases, 3, True, q, node))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = {r: h for r, _, h, _ in (q.get(timeout=120) for _ in range(world))}
@@ -364,3 +380,88 @@ def test_emulated_ranks_match_golden():
             assert h == c["hash"], (c["name"], world, chunks)
             assert [int(v) for v in pen] == c["penalties"]
             assert ready.shape == (world, chunks)
+
+
+class _FakeComm:
+    """seqalign.Comm stand-in for the RCCL rendezvous (no device, no RCCL)."""
+
+    made = []
+
+    def __init__(self, device, uid, world, rank):
+        self.uid, self.world, self.rank = uid, world, rank
+        _FakeComm.made.append(self)
+
+    @staticmethod
+    def unique_id():
+        return bytes(range(128))
+
+    def barrier(self):
+        pass
+
+    def close(self):
+        pass
+
+
+def test_rccl_rendezvous_stale_file_timeout_and_length(tmp_path, monkeypatch):
+    """dist.rccl_comm's id rendezvous with a fake communicator: a file left by
+    an earlier run (older than this rank's start) is never used, a short file
+    is waited past, a missing id times out, and rank 0's fresh id is taken."""
+    import sys
+    import time
+
+    sys.path.insert(0, PKG)
+    import dist as nwdist
+    import seqalign
+
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    monkeypatch.setenv("NWK_RUN_ID", "rdvtest")
+    monkeypatch.setenv("MASTER_PORT", "4242")
+    monkeypatch.setattr(seqalign, "Comm", _FakeComm)
+    path = tmp_path / ("nwk_rccl_id_%s" % nwdist.run_key())
+    # a stale id from a run that died: ignored, so rank 1 times out
+    path.write_bytes(b"\x07" * 128)
+    old = time.time() - 3600
+    os.utime(path, (old, old))
+    with pytest.raises(RuntimeError, match="no RCCL id"):
+        nwdist.rccl_comm(0, 2, 1, timeout_s=0.3)
+    # a fresh but short file (rank 0 mid-write): waited past, then timeout
+    path.write_bytes(b"\x07" * 100)
+    with pytest.raises(RuntimeError, match="no RCCL id"):
+        nwdist.rccl_comm(0, 2, 1, timeout_s=0.3)
+    # rank 0 writes its id (and removes the file after the barrier); rank 1 reads a fresh one
+    c0 = nwdist.rccl_comm(0, 2, 0)
+    assert c0.rank == 0 and _FakeComm.made[-1].uid == bytes(range(128)) and not path.exists()
+    path.write_bytes(bytes(range(128)))
+    c1 = nwdist.rccl_comm(0, 2, 1, timeout_s=5)
+    assert c1.rank == 1 and _FakeComm.made[-1].uid == bytes(range(128))
+    assert nwdist.read_rendezvous_id(str(path), 1, time.time() - 10, 1) == bytes(range(128))
+
+
+def test_node_records_stale_segment_is_replaced():
+    """NodeRecords: rank 0 replaces a segment of the same name left by a run
+    that died; publish / wait round-trips a block (world 1)."""
+    import sys
+    from multiprocessing import shared_memory
+
+    sys.path.insert(0, PKG)
+    import dist as nwdist
+
+    class One:
+        world, rank = 1, 0
+
+        def max(self, x):
+            return x
+
+    key = "t%d" % os.getpid()
+    stale = shared_memory.SharedMemory(name="nwk_rec_" + key, create=True, size=4096)
+    stale.buf[:8] = b"\xff" * 8
+    try:
+        nr = nwdist.NodeRecords(One(), 2, [3, 2], key=key)
+        blk = nwdist.pack_records([5, 6], [10, 11], np.full((2, 64), 9, dtype=np.uint8), 3)
+        nr.publish(0, blk, 7)
+        assert (nr.wait(0, 7, timeout_s=1) == blk).all()
+        with pytest.raises(RuntimeError, match="not published"):
+            nr.wait(1, 7, timeout_s=0.05)
+        nr.close()
+    finally:
+        stale.close()

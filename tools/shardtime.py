@@ -12,7 +12,11 @@ tests/golden/large/<wl>.json, big13: the published answer) before a time is
 printed.  Rank 0's chain (skel:159) is then replayed from the measured
 per-link cost tau of this host's chain (nwk_chain_hash over P records):
     chain_end = max(chain_end, ready of piece c on every rank) + links(c) * tau
-The all-gather of 72-byte records is not emulated (microseconds of transfer).
+The exchange: streamed pieces reach rank 0 through node shared memory as they
+are ready (dist.NodeRecords), and one all-gather (AG_S) follows the last rank's
+launch; the alternative of one RCCL all-gather per piece is replayed too, with
+no piece exchanged before every rank's launch has drained (an RCCL kernel cannot
+start while the persistent fill holds the GPU, profiles/r05/overlap).
 W = 1 is the single-GPU getMinimumPenalties (align_all: batches with the chain
 overlapped), the bench's N=1 step.
 
@@ -74,6 +78,10 @@ print("%s: %d pairs; host chain %.1f ns per link (%.2f ms for all %d links)" % (
 
 es = None
 t1 = None
+# one small all-gather (72-B records of a piece or shard, 8 ranks over xGMI):
+# launch to completion of an RCCL-shaped kernel on an idle GPU was 0.08 ms
+# (profiles/r05/overlap); the transfer is kilobytes
+AG_S = float(os.environ.get("NWK_ST_AG_MS", "0.1")) * 1e-3
 for W in [int(a) for a in args] or [1, 2, 4, 8]:
     if W == 1:
         best = 1e9
@@ -112,12 +120,23 @@ for W in [int(a) for a in args] or [1, 2, 4, 8]:
         parts, _ = nwdist.chunk_parts(lens, r, W, C)
         for c in range(C):
             links[c] += len(parts[c])
+    # pieces reach rank 0 as they are ready (node shared memory, dist.NodeRecords:
+    # microseconds), then ONE all-gather once every rank's launch has drained
     end = 0.0
     for c in range(C):
         end = max(end, ready[:, c].max()) + links[c] * tau
     fill_done = ready[:, -1].max()
+    end = max(end, fill_done + AG_S)
+    # one RCCL all-gather per piece instead: an RCCL kernel cannot start while a
+    # rank's persistent fill launch holds the GPU (profiles/r05/overlap), so no
+    # piece is exchanged before that rank's launch has drained (its last piece)
+    end_rccl = 0.0
+    for c in range(C):
+        end_rccl = max(end_rccl, max(ready[r, c] if not stream else ready[r, -1] for r in range(W)) + AG_S) + links[c] * tau
     slow = int(np.argmax(ready[:, -1]))
     print("%s W=%d, %d piece(s)%s: slowest rank %d ready at %.2f ms (pieces %s ms); chain ends %.2f ms (exposed %.2f ms)%s;"
-          " answer ok" % (wl, W, C, " streamed" if stream else "", slow, fill_done * 1e3,
-                          " ".join("%.2f" % (x * 1e3) for x in ready[slow]), end * 1e3, (end - fill_done) * 1e3,
-                          "  speedup vs W=1: %.2fx" % (t1 / end) if t1 else ""), flush=True)
+          " with an RCCL all-gather per piece %.2f ms%s; answer ok" % (
+              wl, W, C, " streamed" if stream else "", slow, fill_done * 1e3,
+              " ".join("%.2f" % (x * 1e3) for x in ready[slow]), end * 1e3, (end - fill_done) * 1e3,
+              "  speedup vs W=1: %.2fx" % (t1 / end) if t1 else "", end_rccl * 1e3,
+              " (%.2fx)" % (t1 / end_rccl) if t1 else ""), flush=True)
