@@ -50,7 +50,10 @@ namespace {
 //            code of column s_half - 32 lane + q)
 //   H, V     h and v planes of the previous step
 //   cons     LDS: band-above row, entry (column & 63) * NP + k (bit 31)
-//   ring     LDS: this band's last row, entry (column & 127) * NP + k (bit 31)
+//   ring     LDS: this band's last row at this block's entries: step s0 + q writes entry
+//            q + 1 (the caller passes the ring + ((s0 & 127) * NP): entry (s & 127) + 1
+//            holds column s - 2047, so column c is at entry ((c - 1) & 127) + 1 -- immediate
+//            offsets from one address per block, no per-step address arithmetic)
 //   eh       MASK blocks: this lane's bit-0 column at step s0 (columns < 0 keep
 //            v = 0; strips: the column within the current row pass, so a bit
 //            entering column 0 of its next pass sees the left border)
@@ -143,7 +146,7 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
     }
     if constexpr (PROD) {  // lane 63 bit 31 = the band's last row at column s - 2047
       if (lane == 63) {
-        unsigned* e = ring + ((s + 1) & 127) * NP;
+        unsigned* e = ring + (q + 1) * NP;
         if constexpr (NP == 4) *reinterpret_cast<uint4*>(e) = make_uint4(H[0], H[1], H[2], H[3]);
         else *reinterpret_cast<uint2*>(e) = make_uint2(H[0], H[1]);
       }
@@ -575,7 +578,7 @@ __device__ __forceinline__ void trace_bits(const FillArgs& a, const PairDesc& pd
 template <int NP, int SR, bool FUSE>
 __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned cons_all[4][64 * NP];
-  __shared__ __attribute__((aligned(16))) unsigned ring_all[4][128 * NP];
+  __shared__ __attribute__((aligned(16))) unsigned ring_all[4][129 * NP];
   __shared__ __attribute__((aligned(16))) unsigned char obuf_all[4][kTraceRing];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -684,9 +687,11 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
 
       const bool mask = sb < 32;
       const bool prod = to_below && sb >= 31;
+      unsigned* const ring_sb = ring + ((64 * sb) & 127) * NP;
 #pragma unroll
       for (int blk = 0; blk < 8; ++blk) {
         const int s0 = 64 * sb + 8 * blk;
+        unsigned* const rblk = ring_sb + 8 * blk * NP;  // (s0 & 127) = (64 sb & 127) + 8 blk
         const unsigned w0 = blk < 4 ? wa0 : wb0, w1 = blk < 4 ? wa1 : wb1;
         const int rel = (s0 >> 3) - blo;
         const bool sto = (unsigned)rel < (unsigned)nblk;
@@ -695,11 +700,11 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
         bool ls = true;
         if (lwin) ls = bits_lane_stored(hi0 + (int64_t)s0 * pd.m, lim, hlim);
         if (mask) {
-          if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
-          else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
+          if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls);
+          else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls);
         } else {
-          if (prod) bits_block<NP, SR, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
-          else bits_block<NP, SR, false, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
+          if (prod) bits_block<NP, SR, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls);
+          else bits_block<NP, SR, false, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls);
         }
         if ((blk & 3) == 3) {  // end of a 32-step half: its window becomes the previous one
           yp0 = w0;
@@ -712,7 +717,7 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
         const int q = sb - 32;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        const unsigned* e = ring + ((64 * q + lane) & 127) * NP;
+        const unsigned* e = ring + ((((64 * q + lane) - 1) & 127) + 1) * NP;
         unsigned val = 0;
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
@@ -796,7 +801,7 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
 template <int NP, int SR, bool FUSE>
 __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned cons_all[4][64 * NP];
-  __shared__ __attribute__((aligned(16))) unsigned ring_all[4][128 * NP];
+  __shared__ __attribute__((aligned(16))) unsigned ring_all[4][129 * NP];
   __shared__ __attribute__((aligned(16))) unsigned char obuf_all[4][kTraceRing];
   extern __shared__ __attribute__((aligned(16))) unsigned hand_all[];  // [4][a.strip_ring]
   const int lane = threadIdx.x & 63;
@@ -889,9 +894,11 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
 
       const bool mask = q0 < 32;  // some lane's bit 0 enters a pass in this super-block
       const bool prod = sb >= 31;
+      unsigned* const ring_sb = ring + ((64 * sb) & 127) * NP;
 #pragma unroll
       for (int blk = 0; blk < 8; ++blk) {
         const int s0 = 64 * sb + 8 * blk;
+        unsigned* const rblk = ring_sb + 8 * blk * NP;  // (s0 & 127) = (64 sb & 127) + 8 blk
         const unsigned w0 = blk < 4 ? wa0 : wb0, w1 = blk < 4 ? wa1 : wb1;
         const int uh = blk < 4 ? ua : ub;
         if ((blk & 3) == 0 && mask) {  // this lane's bit 0 enters pass >= 1 here: switch the row codes
@@ -915,11 +922,11 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
         bool ls = true;
         if (lwin) ls = bits_lane_stored((int64_t)(eh + 7) * pd.m + negRn, lim, hlim);
         if (mask) {
-          if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
-          else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
+          if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls);
+          else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls);
         } else {
-          if (prod) bits_block<NP, SR, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
-          else bits_block<NP, SR, false, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, ring, st, sto, eh, ls);
+          if (prod) bits_block<NP, SR, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls);
+          else bits_block<NP, SR, false, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls);
         }
         if ((blk & 3) == 3) {  // end of a 32-step half: its window becomes the previous one
           yp0 = w0;
@@ -933,7 +940,7 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_strip(FillArgs a) {
       if (sb >= 32) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        const unsigned* e = ring + ((64 * sb + lane) & 127) * NP;
+        const unsigned* e = ring + ((((64 * sb + lane) - 1) & 127) + 1) * NP;
         unsigned val = 0;
 #pragma unroll
         for (int k = 0; k < NP; ++k) {

@@ -940,15 +940,23 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
   }
 }
 
-// Waves per SIMD the kernel is compiled for (NWK_COL_WPE; register budget 512 / WPE)
+// Waves per SIMD the kernel is compiled for (register budget 512 / WPE): the
+// fused-finalize instantiation at NWK_COL_WPE (4); the plain one at 4 or, for
+// jobs of a few rounds of bands (launch_col's wpe), NWK_COL_WPE_HI (5, <= 96
+// VGPRs, a few spills outside the step loop): C3's 4-rank shard (3.1 rounds of
+// 4,096 slots) 60.5 -> 48.6 ms, the 8-rank one 32.2 -> 30.5 ms, big13 equal;
+// the streamed fused ranks (C4 W = 8) are faster at 4 (22.0 vs 24.5 ms)
+// (profiles/r05/ab/col_wpe.txt).
 #ifndef NWK_COL_WPE
 #define NWK_COL_WPE 4
 #endif
-#define NWK_COL_OCC __attribute__((amdgpu_waves_per_eu(NWK_COL_WPE)))
+#ifndef NWK_COL_WPE_HI
+#define NWK_COL_WPE_HI 5
+#endif
 
 // FUSE: the instantiation with the fused finalize (FillArgs::fuse_fin)
-template <int NP, int SR, bool FUSE>
-__global__ __launch_bounds__(256) NWK_COL_OCC void nw_align_col(FillArgs a) {
+template <int NP, int SR, bool FUSE, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void nw_align_col(FillArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char obuf_all[4][kTraceRing];
   __shared__ __attribute__((aligned(16))) unsigned pf_all[4][512];  // trace_col's tile ahead (LDS-DMA)
   const int lane = threadIdx.x & 63;
@@ -978,8 +986,13 @@ __global__ __launch_bounds__(256) NWK_COL_OCC void nw_align_col(FillArgs a) {
     const int band = task.y;
     const int R0 = band * kBR;
     // the longest spans of a span-bound batch issue ahead of the other fill waves
-    if (pd.prio >= 2) __builtin_amdgcn_s_setprio(2);
-    else if (pd.prio == 1) __builtin_amdgcn_s_setprio(1);
+    // (band_prio: a pair's bands run as a pipeline at the pace of its slowest
+    // upstream band, so the upper bands issue first -- 3 .. 0 by quarter of the pair)
+    const int bprio = a.band_prio ? 3 - (4 * band) / pd.nbands : 0;
+    const int prio = pd.prio > bprio ? pd.prio : bprio;
+    if (prio >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (prio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (prio == 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
     // code bit planes of rows R0 + 32 lane + b (rows past m: code 0, never traced)
     unsigned x0 = 0, x1 = 0;
@@ -1141,23 +1154,24 @@ __global__ __launch_bounds__(256) NWK_COL_OCC void nw_align_col(FillArgs a) {
 }
 
 template <int NP, int SR>
-hipError_t col_launch(const FillArgs& a, int grid, hipStream_t s) {
+hipError_t col_launch(const FillArgs& a, int grid, bool hi, hipStream_t s) {
 #ifdef NWK_COL_NOFUSE
   if (a.fuse_fin) return hipErrorInvalidValue;
 #else
-  if (a.fuse_fin) hipLaunchKernelGGL((nw_align_col<NP, SR, true>), dim3(grid), dim3(256), 0, s, a);
+  if (a.fuse_fin) hipLaunchKernelGGL((nw_align_col<NP, SR, true, NWK_COL_WPE>), dim3(grid), dim3(256), 0, s, a);
   else
 #endif
-  hipLaunchKernelGGL((nw_align_col<NP, SR, false>), dim3(grid), dim3(256), 0, s, a);
+  if (hi) hipLaunchKernelGGL((nw_align_col<NP, SR, false, NWK_COL_WPE_HI>), dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((nw_align_col<NP, SR, false, NWK_COL_WPE>), dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 template <int NP, int SR>
-int col_occ() {
+int col_occ(bool hi) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&nw_align_col<NP, SR, false>), 256, 0) !=
-      hipSuccess)
-    return 1;
+  const void* k = hi ? reinterpret_cast<const void*>(&nw_align_col<NP, SR, false, NWK_COL_WPE_HI>)
+                     : reinterpret_cast<const void*>(&nw_align_col<NP, SR, false, NWK_COL_WPE>);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, 256, 0) != hipSuccess) return 1;
   return n > 0 ? n : 1;
 }
 
@@ -1165,32 +1179,32 @@ int col_occ() {
 
 int bits_sr(int pxy, int pgap);
 
-hipError_t launch_col(const FillArgs& a, int pxy, int pgap, int grid, hipStream_t s) {
+hipError_t launch_col(const FillArgs& a, int pxy, int pgap, int grid, bool hi, hipStream_t s) {
   const int sr = bits_sr(pxy, pgap);
 #ifdef NWK_COL_ONE  // (development: one instantiation, fast builds)
-  return pgap == 2 && sr == 1 ? col_launch<4, 1>(a, grid, s) : hipErrorInvalidValue;
+  return pgap == 2 && sr == 1 ? col_launch<4, 1>(a, grid, hi, s) : hipErrorInvalidValue;
 #endif
   if (pgap == 1) {
     switch (sr) {
-      case -1: return col_launch<2, -1>(a, grid, s);
-      case 0: return col_launch<2, 0>(a, grid, s);
-      case 1: return col_launch<2, 1>(a, grid, s);
-      default: return col_launch<2, 2>(a, grid, s);
+      case -1: return col_launch<2, -1>(a, grid, hi, s);
+      case 0: return col_launch<2, 0>(a, grid, hi, s);
+      case 1: return col_launch<2, 1>(a, grid, hi, s);
+      default: return col_launch<2, 2>(a, grid, hi, s);
     }
   }
   if (pgap == 2) {
     switch (sr) {
-      case -1: return col_launch<4, -1>(a, grid, s);
-      case 0: return col_launch<4, 0>(a, grid, s);
-      case 1: return col_launch<4, 1>(a, grid, s);
-      case 2: return col_launch<4, 2>(a, grid, s);
-      case 3: return col_launch<4, 3>(a, grid, s);
-      default: return col_launch<4, 4>(a, grid, s);
+      case -1: return col_launch<4, -1>(a, grid, hi, s);
+      case 0: return col_launch<4, 0>(a, grid, hi, s);
+      case 1: return col_launch<4, 1>(a, grid, hi, s);
+      case 2: return col_launch<4, 2>(a, grid, hi, s);
+      case 3: return col_launch<4, 3>(a, grid, hi, s);
+      default: return col_launch<4, 4>(a, grid, hi, s);
     }
   }
   return hipErrorInvalidValue;
 }
 
-int col_blocks_per_cu(int pgap) { return pgap == 1 ? col_occ<2, 1>() : col_occ<4, 1>(); }
+int col_blocks_per_cu(int pgap, bool hi) { return pgap == 1 ? col_occ<2, 1>(hi) : col_occ<4, 1>(hi); }
 
 }  // namespace nwk

@@ -148,6 +148,7 @@ struct FillArgs {
   int go, ge;              // kAffine: gap open / extend
   int dbg_notrace;         // debug: skip the affine traceback
   int dbg_badwalk;         // debug (tests): slot + 1 whose nw_align_col walk reports itself failed (err 16)
+  int band_prio;           // kCol: issue priority by band (upstream bands first): 0 off, 1 on
   int lin_mode;            // nw_align: 0 normal, 1 linear-space fill pass, 2 linear-space group recompute + trace
   unsigned* prog;          // debug: per-wave progress markers (NWK_WATCHDOG)
   unsigned* tdone;         // kPacked2: per task, 1 = filled and released
@@ -221,8 +222,9 @@ int bits_blocks_per_cu(int pgap);
 hipError_t launch_strip(const FillArgs& a, int pxy, int pgap, int grid, hipStream_t s);
 int strip_blocks_per_cu(int pgap, int ring_dwords);
 // kCol (nwk_col.hip)
-hipError_t launch_col(const FillArgs& a, int pxy, int pgap, int grid, hipStream_t s);
-int col_blocks_per_cu(int pgap);
+// hi: the plain instantiation at NWK_COL_WPE_HI waves per SIMD (not with fuse_fin)
+hipError_t launch_col(const FillArgs& a, int pxy, int pgap, int grid, bool hi, hipStream_t s);
+int col_blocks_per_cu(int pgap, bool hi = false);
 // kGotoh (nwk_gotoh.hip): instantiated for a fixed set of (pxy, go, ge)
 bool gotoh_admissible(int pxy, int go, int ge, int alpha);
 int gotoh_granules(int go, int ge);  // granules per 32-column chunk of a band's last row

@@ -1454,6 +1454,24 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       const double est_dev = (maxlen / 128.0) * 0.007 * std::max(1.0, waves / slots);
       const double est_host = bytes / (350e3 * c->host_threads);
       devhash = fin_mode == 1 || est_dev < 0.8 * est_host;
+      // nw_align_col under "auto": the device finalize runs after the launch (a
+      // row's SHA-512 is one lane's serial chain: ~4.4 ms for C3's 100 KB rows),
+      // while the streamed host finalize (hstream below) takes each pair as its
+      // walk ends, during the launch -- only the last pair's ~0.3 ms is left
+      // after it.  So host threads finalize wherever they keep up with the fill
+      // (estimated: cells at ~30 TCUPS, or the longest pair's span at ~0.27 us
+      // per step): C3's 8-rank shard 35 -> ~31 ms; C4 (1 GB of rows) stays on
+      // the device.
+      static const int hstream_auto = getenv("NWK_HOST_STREAM") ? atoi(getenv("NWK_HOST_STREAM")) : 1;
+      if (devhash && fin_mode < 0 && pl.mode == kCol && hstream_auto != 0) {
+        double cells = 0, span = 0;
+        for (size_t q = pos; q < end; ++q) {
+          cells += (double)dp[q].m * dp[q].n;
+          span = std::max(span, (double)dp[q].n + 100.0 * (double)ceil_div(dp[q].m, kBitsRows));
+        }
+        const double est_fill = std::max(cells / 3.0e10, span * 0.27e-3);
+        if (est_host < 0.5 * est_fill) devhash = false;
+      }
       st.device_finalized += devhash ? 1 : 0;
     }
     // Layout: [granules | slack | matrices | op strings].  The granule region
@@ -1656,6 +1674,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.go = sc.go;
     fa.dbg_notrace = (getenv("NWK_AFF_NOTRACE") || getenv("NWK_NOTRACE")) ? 1 : 0;
     fa.dbg_badwalk = getenv("NWK_DBG_BADWALK") ? atoi(getenv("NWK_DBG_BADWALK")) : 0;
+    static const int band_prio_env = getenv("NWK_BAND_PRIO") ? atoi(getenv("NWK_BAND_PRIO")) : 0;
+    fa.band_prio = band_prio_env;
     fa.lin_mode = 0;
     fa.prog = nullptr;
     fa.yw = bitsy || gotoh ? c->d_yw.as<unsigned>() : nullptr;
@@ -1767,8 +1787,14 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     if (pl.mode == kBits)
       HIP_TRY(launch_bits(fa, sc.pxy, sc.pgap, (int)std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
-    else if (pl.mode == kCol)
-      HIP_TRY(launch_col(fa, sc.pxy, sc.pgap, (int)std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
+    else if (pl.mode == kCol) {
+      // the plain (not fused) instantiation at 5 waves/SIMD (nwk_col.hip
+      // NWK_COL_WPE_HI): C3's 4-rank shard 60.5 -> 48.6 ms; NWK_COL_WPE_HI=0: 4
+      static const int wpe_hi_env = getenv("NWK_COL_WPE_HI") ? atoi(getenv("NWK_COL_WPE_HI")) : 1;
+      const bool hi = !fuse && wpe_hi_env != 0;
+      const int gcol = col_blocks_per_cu(sc.pgap, hi) * c->cus;
+      HIP_TRY(launch_col(fa, sc.pxy, sc.pgap, (int)std::min<int64_t>(gcol, ceil_div(ntasks, 4)), hi, c->stream));
+    }
     else if (pl.mode == kBitsStrip)
       HIP_TRY(launch_strip(fa, sc.pxy, sc.pgap, (int)std::min<int64_t>(grid, ceil_div(ntasks, 4)), c->stream));
     else if (gotoh)
