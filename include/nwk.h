@@ -58,8 +58,11 @@ typedef struct nwk_opts {
   int64_t workspace_bytes;   /* HBM budget per device; 0 = 92% of free memory */
   int32_t verbose;           /* 1 = per-call statistics on stderr */
   int32_t finalize;          /* pair finalize (rows, penalty, SHA-512): 0 auto, 1 host, 2 device (nw_rows + nw_hash
-                                after each fill launch), 3 device fused into the nw_align_bits / nw_align_strip launch:
-                                each pair's record reaches the host as soon as it is hashed (nwk_align_pairs_poll) */
+                                after each fill launch), 3 device fused into the nw_align_bits / nw_align_strip /
+                                nw_align_col launch: each pair's record reaches the host as soon as it is hashed
+                                (nwk_align_pairs_poll).  Auto fuses nw_align_col batches of >= 8,192 pairs in a
+                                chained call, and streams nw_align_col pairs to host threads during the launch where
+                                the host keeps up with the fill */
   int32_t linear_space;      /* linear-space traceback: 0 = only for pairs whose matrix exceeds
                                 the HBM budget, -1 = never, G > 0 = every pair, G bands per recompute group */
   int32_t kernel;            /* linear fill kernel: 0 auto (where admissible -- pxy >= 0, pgap 1 or 2, <= 4
@@ -70,7 +73,11 @@ typedef struct nwk_opts {
                                 3 nw_align_pk2, 4 nw_align_bits band tasks, 5 nw_align_strip wherever admissible
                                 (n / 64 in [63, 200] for pgap 2, [63, 500] for pgap 1), 6 nw_align_col (bit-parallel
                                 columns, nw_align_bits' domain; a kernel where it is not exact -- W > 4, mixed-sign K,
-                                pgap > 2 -- falls back) */
+                                pgap > 2 -- falls back), 7 nw_align_gotoh for the affine calls (bit-sliced Gotoh
+                                planes; instantiated scorings only, else nw_align_pka / nw_align_affine).  Affine
+                                calls under 0 take nw_align_gotoh where instantiated and <= 4 symbols, else
+                                nw_align_pka where its int16 window holds, else nw_align_affine; 1 pins
+                                nw_align_affine, 2 / 3 nw_align_pka */
   int32_t collective;        /* nwk_get_minimum_penalties: 1 = take the sharded RCCL all-gather path even when
                                 ngpus == 1 (one communicator of one rank; tests the collective on a 1-GPU box) */
   int32_t task_order;        /* nw_align_bits band tasks: 0 auto (band-major above one round of wave slots), 1 pair-major
@@ -87,7 +94,9 @@ typedef struct nwk_stats {
   int32_t batches;           /* workspace batches used */
   int32_t bits;              /* storage width used */
   int32_t mode;              /* 0 = profile, 1 = compare, 2 = literal, 3 = affine, 4 = packed profile, 5 = packed band
-                                pairs, 7 = packed affine band pairs, 8 = bit-sliced planes, 9 = bit-sliced strips */
+                                pairs, 7 = packed affine band pairs, 8 = bit-sliced planes (nw_align_bits), 9 =
+                                bit-sliced strips (nw_align_strip), 10 = bit-parallel columns (nw_align_col), 11 =
+                                bit-sliced affine planes (nw_align_gotoh) */
   int32_t fill_launches;     /* fill-kernel launches in the call */
   int32_t device_finalized;  /* batches whose pairs were finalized on the device */
   int32_t linear_space_pairs; /* pairs aligned with the linear-space traceback */

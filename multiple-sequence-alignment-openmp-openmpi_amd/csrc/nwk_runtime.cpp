@@ -1168,7 +1168,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         bands += ceil_div(w.m, kBitsRows);
         maxlen = std::max(maxlen, std::max(w.m, w.n));
       }
-      const double slots = 4.0 * col_blocks_per_cu(sc.pgap) * c->cus;
+      const double slots = 4.0 * col_blocks_per_cu(sc.pgap, true) * c->cus;  // (plain launches: 5 waves/SIMD)
       col = bands > 0 && (bands <= 3.0 * slots || maxlen <= 16384);
     }
     if (col) pl.mode = kCol;
