@@ -1150,27 +1150,19 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     const int want = c->opts.kernel == 5 ? 1 : c->opts.kernel == 4 ? 0 : strip_env;
     if (want != 0 && use_strips(c, work, sc.pgap, want == 1, &strip_ring)) pl.mode = kBitsStrip;
   }
-  // nw_align_col under "auto": a pair costs its span n + ~100 per band there
-  // against n + 2112 per band for nw_align_bits, and its stores are windowed
-  // (write-bound jobs), so it wins wherever the job is not many rounds of long
-  // bands: big13 24.1 vs 33 ms per step, C4 91 vs 100 ms, C3's 8-rank shard
-  // 34 vs 47 ms; C3 on one GPU (12 rounds of 50k-column bands) stays with
-  // nw_align_bits (153 vs 160 ms).  NWK_COL=0/1 forces (A/B runs).
+  // nw_align_col under "auto", wherever the bits kernels apply: a pair costs its
+  // span n + ~100 per band there against n + 2112 per band for nw_align_bits,
+  // its stores are windowed (write-bound jobs), its plain launches run 5
+  // waves/SIMD and its pairs stream to the host finalize during the launch.
+  // big13 24.1 vs 33 ms per step, C4 85 vs 100 ms, C3's 8 / 4 / 2-rank shards
+  // 30 / 47 / 83 vs 47 / 61 / 97 ms, and since round 5 C3 on one GPU too
+  // (155.2 vs 160.9 ms per step, profiles/r05/ab/c3_col_vs_bits.txt; round 4 at
+  // 4 waves/SIMD and a device finalize after the launch: 160 vs 153 ms).
+  // NWK_COL=0 keeps nw_align_bits (A/B runs), NWK_STRIP=1 forces strips.
   if ((pl.mode == kBits || pl.mode == kBitsStrip) && c->opts.kernel == 0) {
     static const int col_env = getenv("NWK_COL") ? atoi(getenv("NWK_COL")) : -1;
     static const bool strip_forced = getenv("NWK_STRIP") && atoi(getenv("NWK_STRIP")) == 1;
-    bool col = col_env == 1;
-    if (col_env < 0 && !strip_forced) {
-      int64_t bands = 0;
-      int maxlen = 0;
-      for (const auto& w : work) {
-        if (w.m <= 0 || w.n <= 0) continue;
-        bands += ceil_div(w.m, kBitsRows);
-        maxlen = std::max(maxlen, std::max(w.m, w.n));
-      }
-      const double slots = 4.0 * col_blocks_per_cu(sc.pgap, true) * c->cus;  // (plain launches: 5 waves/SIMD)
-      col = bands > 0 && (bands <= 3.0 * slots || maxlen <= 16384);
-    }
+    const bool col = col_env == 1 || (col_env < 0 && !strip_forced);
     if (col) pl.mode = kCol;
   }
   const bool bitsy = pl.mode == kBits || pl.mode == kBitsStrip || pl.mode == kCol;
