@@ -29,9 +29,10 @@
 // blocks within bits_w columns of the diagonal when windowed.
 //
 // Traceback: the wave that finishes a pair's last band walks the three-state
-// walk from (m, n) on the scalar unit over tiles of 64 steps x 128 rows held
-// in VGPRs (lane L = step 32 k + L, four row-lanes x four words), one
-// v_readlane per word per move; a gap's first column is emitted as 'u' / 'l'
+// walk from (m, n) on the scalar unit over tiles of 128 steps x 64 rows held
+// in VGPRs (lane L = steps 64 u + L and 64 u + 64 + L, two row-lanes x four
+// words), the next tile along the diagonal prefetched, one v_readlane per word
+// per move; a gap's first column is emitted as 'u' / 'l'
 // (the finalize charges go + ge there, ge elsewhere).  A cell outside the
 // stored blocks flags the pair for a wider re-run (FillArgs::retry).
 #include "nwk_bits_dev.h"
@@ -93,98 +94,184 @@ __device__ __noinline__ u64 gran_wait(const u64* p, unsigned epoch, u64 v, unsig
 struct Walk {
   int i, j, st, k;  // cell, state (0 H, 1 F, 2 E), moves emitted
   int b, q;         // bit of the cell's row in its row-lane, tile lane of its step
-  unsigned acc;     // moves (k & ~3) .. k - 1, one byte each
 };
 
-// one move out of the walk: byte k of the reversed move string (flushed 256 B
-// at a time from the VGPR outv, one dword per lane)
-__device__ __forceinline__ void walk_emit(Walk& w, unsigned mv, unsigned& outv, unsigned* ops, int lane) {
-  w.acc |= mv << (8 * (w.k & 3));
-  if ((w.k & 3) == 3) {
-    outv = lane == ((w.k >> 2) & 63) ? w.acc : outv;
-    w.acc = 0;
-    if ((w.k & 255) == 255) ops[(int64_t)(w.k >> 8) * 64 + lane] = outv;
-  }
-  ++w.k;
-}
-
-// Moves inside row-lane H of the tile (oracle/nw_oracle.c:241-256): returns when
-// the walk reaches row or column 0, leaves the row-lane (b < 0) or the tile's
-// steps (q < qmin), or has emitted kcap moves.
-template <int H>
-__device__ __forceinline__ void walk_rl(const unsigned (&tw)[4][4], Walk& w, int qmin, int kcap, unsigned& outv,
-                                        unsigned* ops, int lane) {
-  for (;;) {
-    if (w.i == 0 || w.j == 0 || w.q < qmin || w.k >= kcap) return;
-    const unsigned dD = (unsigned)__builtin_amdgcn_readlane((int)tw[H][0], w.q);
-    const unsigned dF = (unsigned)__builtin_amdgcn_readlane((int)tw[H][1], w.q);
-    unsigned mv;
-    if (w.st == 0 && ((dD >> w.b) & 1u)) {
-      mv = 'D';
-      --w.i;
-      --w.j;
-      --w.b;
-      w.q -= 2;
-    } else {
-      if (w.st == 0) w.st = ((dF >> w.b) & 1u) ? 1 : 2;
-      if (w.st == 1) {  // F: an UP move; back to H where the gap opened (open wins ties)
-        const unsigned dX = (unsigned)__builtin_amdgcn_readlane((int)tw[H][3], w.q);
-        const bool ext = (dX >> w.b) & 1u;
-        mv = ext ? 'U' : 'u';
-        w.st = ext ? 1 : 0;
-        --w.i;
-        --w.b;
-        --w.q;
-      } else {  // E: a LEFT move
-        const unsigned dE = (unsigned)__builtin_amdgcn_readlane((int)tw[H][2], w.q);
-        const bool ext = (dE >> w.b) & 1u;
-        mv = ext ? 'L' : 'l';
-        w.st = ext ? 2 : 0;
-        --w.j;
-        --w.q;
-      }
+// n copies of move c: bytes k .. k + n - 1 of the reversed move string, staged
+// in the VGPR outv (lane L holds bytes 4 L .. 4 L + 3 of the current 256) and
+// flushed 256 B at a time
+__device__ __forceinline__ void emit_run(Walk& w, unsigned c, int n, unsigned& outv, unsigned* ops, int lane) {
+  const unsigned rep = c * 0x01010101u;
+  while (n > 0) {
+    const int kk = w.k & 255, m = n < 256 - kk ? n : 256 - kk;
+    int lo = kk - 4 * lane, hi = kk + m - 4 * lane;
+    lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
+    hi = hi < 0 ? 0 : (hi > 4 ? 4 : hi);
+    outv |= rep & (unsigned)(((1ull << (8 * hi)) - 1) ^ ((1ull << (8 * lo)) - 1));
+    w.k += m;
+    n -= m;
+    if ((w.k & 255) == 0) {
+      ops[(int64_t)((w.k >> 8) - 1) * 64 + lane] = outv;
+      outv = 0;
     }
-    walk_emit(w, mv, outv, ops, lane);
-    if (w.b < 0) return;
   }
 }
 
-__device__ __noinline__ void trace_gotoh(const FillArgs& a, const PairDesc& pd, int lane) {
-  Walk w{pd.m, pd.n, 0, 0, 0, 0, 0u};
+// A walk tile: row-lanes 2 g, 2 g + 1 of a band (rows 64 g .. + 63) by steps
+// 64 u .. 64 u + 127.  A diagonal run crosses it corner to corner (two steps
+// per row), so a tile serves ~64 moves; while the walk crosses one, the tile
+// it is predicted to enter next is already loading (gtile_load into nx, copied
+// to tw at the switch).
+struct GKey {
+  int band, g, u;
+};
+
+__device__ __forceinline__ GKey gkey_of(int i, int j) {
+  const int r = i - 1, rl = r & (kBR - 1), s = j + rl;
+  return GKey{r >> 11, rl >> 6, s >= 128 ? (s >> 6) - 1 : 0};
+}
+
+// nx[p][h][w]: lane L's word w of row-lane 2 g + h at step 64 u + 64 p + L.  In
+// the 4-step block layout a uint4 holds row-lane 2 g at an even / odd step in
+// x / y and row-lane 2 g + 1 in z / w; a lane loads only its parity's two dwords.
+__device__ __forceinline__ void gtile_load(const FillArgs& a, const PairDesc& pd, GKey k, int lane,
+                                           unsigned (&nx)[2][2][4]) {
+  const int nblk = pd.bits_nblk, blo = gotoh_blk_lo(k.band, pd.m, pd.n, pd.bits_w);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int ss = 64 * k.u + 64 * p + lane;
+    int rel = (ss >> 2) - blo;
+    rel = rel < 0 ? 0 : (rel >= nblk ? nblk - 1 : rel);  // (steps outside the stored blocks are never read)
+    const unsigned* bp =
+        a.mat + pd.mat_off + ((int64_t)k.band * nblk + rel) * 1024 + (ss & 2) * 64 + 4 * k.g + (lane & 1);
+#pragma unroll
+    for (int wd = 0; wd < 4; ++wd) {
+      nx[p][0][wd] = bp[wd * 256];
+      nx[p][1][wd] = bp[wd * 256 + 2];
+    }
+  }
+}
+
+// Moves inside row-lane h = H, step part P of the tile (oracle/nw_oracle.c:241-256),
+// one run at a time: the cell's words are lane q - 64 P (q = its step - 64 u),
+// and every cell a run can reach inside the part is one lane, so a ballot finds
+// where it breaks (a move at a time ran ~550 cycles a move; runs average ~5.5
+// moves on C5).  Returns when the walk reaches row or column 0, leaves the
+// row-lane (b < 0) or the part (q < qlo), or has emitted kcap moves.
+//   H: D while the D bit is set (diagonal: lane -2, bit -1); at the first cell
+//      without it the F-source bit picks F or E (no move yet);
+//   F: UP moves (lane -1, bit -1), 'U' while the F-extend bit is set, then 'u'
+//      back to H; E: the same leftwards (lane -1, same bit) on the E-extend bit.
+template <int H, int P>
+__device__ __forceinline__ void walk_rl(const unsigned (&tw)[2][2][4], Walk& w, int qlo, int kcap, unsigned& outv,
+                                        unsigned* ops, int lane) {
+  const int lo = qlo - 64 * P;  // lowest tile lane the part may read
+  while (w.i > 0 && w.j > 0 && w.q >= qlo && w.k < kcap && w.b >= 0) {
+    const int ql = w.q - 64 * P, b = w.b, dl = ql - lane;
+    const int room = kcap - w.k;
+    if (w.st == 0) {
+      const int t = dl >> 1;
+      const bool ok = dl >= 0 && !(dl & 1) && t <= b && lane >= lo;
+      const unsigned bit = (tw[P][H][0] >> ((unsigned)(b - t) & 31u)) & 1u;
+      const u64 brk = __ballot(ok && !bit);
+      const int tlim = (b < ((ql - lo) >> 1) ? b : (ql - lo) >> 1) + 1;
+      const int ts = brk ? (ql - (63 - __builtin_clzll(brk))) >> 1 : tlim;
+      int cap = w.i < w.j ? w.i : w.j;
+      cap = cap < room ? cap : room;
+      const int n = ts < cap ? ts : cap;
+      emit_run(w, 'D', n, outv, ops, lane);
+      w.i -= n;
+      w.j -= n;
+      w.b -= n;
+      w.q -= 2 * n;
+      if (n == ts && ts < tlim) {
+        const unsigned f = (unsigned)__builtin_amdgcn_readlane((int)tw[P][H][1], w.q - 64 * P);
+        w.st = (f >> w.b) & 1u ? 1 : 2;
+      }
+    } else if (w.st == 1) {
+      const bool ok = dl >= 0 && dl <= b && lane >= lo;
+      const unsigned bit = (tw[P][H][3] >> ((unsigned)(b - dl) & 31u)) & 1u;
+      const u64 brk = __ballot(ok && !bit);
+      const int tlim = (b < ql - lo ? b : ql - lo) + 1;
+      const int ts = brk ? ql - (63 - __builtin_clzll(brk)) : tlim;
+      const int cap = w.i < room ? w.i : room;
+      const bool close = ts < tlim && ts < cap;
+      const int n = close ? ts : (tlim < cap ? tlim : cap);
+      emit_run(w, 'U', n, outv, ops, lane);
+      if (close) {
+        emit_run(w, 'u', 1, outv, ops, lane);
+        w.st = 0;
+      }
+      const int mv = n + (close ? 1 : 0);
+      w.i -= mv;
+      w.b -= mv;
+      w.q -= mv;
+    } else {
+      const bool ok = dl >= 0 && lane >= lo;
+      const unsigned bit = (tw[P][H][2] >> (unsigned)b) & 1u;
+      const u64 brk = __ballot(ok && !bit);
+      const int tlim = ql - lo + 1;
+      const int ts = brk ? ql - (63 - __builtin_clzll(brk)) : tlim;
+      const int cap = w.j < room ? w.j : room;
+      const bool close = ts < tlim && ts < cap;
+      const int n = close ? ts : (tlim < cap ? tlim : cap);
+      emit_run(w, 'L', n, outv, ops, lane);
+      if (close) {
+        emit_run(w, 'l', 1, outv, ops, lane);
+        w.st = 0;
+      }
+      const int mv = n + (close ? 1 : 0);
+      w.j -= mv;
+      w.q -= mv;
+    }
+  }
+}
+
+__device__ __forceinline__ void trace_gotoh(const FillArgs& a, const PairDesc& pd, int lane) {
+  Walk w{pd.m, pd.n, 0, 0, 0, 0};
   unsigned outv = 0;
   unsigned* ops = reinterpret_cast<unsigned*>(a.ops + pd.ops_off);
   const int nblk = pd.bits_nblk, kcap = pd.m + pd.n;
-  unsigned tw[4][4];
-  int tband = -1, tgrp = 0, tk = 0, slo = 0, shi = -1;
+  unsigned tw[2][2][4];
+  unsigned nx[2][2][4];
+  GKey cur{-1, 0, 0}, pre{-1, 0, 0};
+  int slo = 0, shi = -1;
   bool out = false;
+  u64 n_sw = 0, n_dem = 0, c_wait = 0;  // (verbose >= 2 timeline: tile switches, demand loads, cycles waiting on tiles)
+  const u64 c0 = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
   while (w.i > 0 && w.j > 0 && w.k < kcap) {
-    const int r = w.i - 1, band = r >> 11, rl = r & (kBR - 1), t = rl >> 5, s = w.j + rl;
-    if (band != tband || (t >> 2) != tgrp || s < 32 * tk || s > 32 * tk + 63) {
-      // tile: steps 32 tk .. + 63 (the cell in its upper half), row-lanes 4 tgrp .. + 3
-      tband = band;
-      tgrp = t >> 2;
-      tk = s >= 64 ? (s >> 5) - 1 : 0;
+    const int r = w.i - 1, band = r >> 11, rl = r & (kBR - 1), g = rl >> 6, s = w.j + rl;
+    if (band != cur.band || g != cur.g || s < 64 * cur.u || s > 64 * cur.u + 127) {
+      // the tile holding the cell: the prefetched one if it does, else loaded now
+      ++n_sw;
+      if (!(band == pre.band && g == pre.g && s >= 64 * pre.u && s <= 64 * pre.u + 127)) {
+        pre = gkey_of(w.i, w.j);
+        gtile_load(a, pd, pre, lane, nx);
+        ++n_dem;
+      }
+      const u64 tw0 = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int wd = 0; wd < 4; ++wd) tw[p][h][wd] = nx[p][h][wd];
+      if (a.stamps) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        c_wait += __builtin_amdgcn_s_memtime() - tw0;
+      }
+      cur = pre;
       const int blo = gotoh_blk_lo(band, pd.m, pd.n, pd.bits_w);
       slo = 4 * blo;
       shi = 4 * (blo + nblk) - 1;
-      const int ss = 32 * tk + lane, rel = (ss >> 2) - blo;
-      if ((unsigned)rel < (unsigned)nblk) {
-        const unsigned* bp = a.mat + pd.mat_off + ((int64_t)band * nblk + rel) * 1024 + (ss & 2) * 64 + 8 * tgrp;
-        const bool od = (ss & 1) != 0;
-#pragma unroll
-        for (int wd = 0; wd < 4; ++wd) {
-          const uint4 p0 = *reinterpret_cast<const uint4*>(bp + wd * 256);
-          const uint4 p1 = *reinterpret_cast<const uint4*>(bp + wd * 256 + 4);
-          tw[0][wd] = od ? p0.y : p0.x;
-          tw[1][wd] = od ? p0.w : p0.z;
-          tw[2][wd] = od ? p1.y : p1.x;
-          tw[3][wd] = od ? p1.w : p1.z;
-        }
+      // the next tile: where a diagonal run from this cell leaves this one (rows
+      // or steps, whichever run out first)
+      const int q = s - 64 * cur.u, ro = rl & 63;
+      const int d = ro + 1 < (q >> 1) + 1 ? ro + 1 : (q >> 1) + 1;
+      if (w.i - d >= 1 && w.j - d >= 1) {
+        pre = gkey_of(w.i - d, w.j - d);
+        gtile_load(a, pd, pre, lane, nx);
       } else {
-#pragma unroll
-        for (int h = 0; h < 4; ++h)
-#pragma unroll
-          for (int wd = 0; wd < 4; ++wd) tw[h][wd] = 0u;
+        pre.band = -1;
       }
     }
     if (s < slo || s > shi) {  // the path left the stored window
@@ -192,20 +279,28 @@ __device__ __noinline__ void trace_gotoh(const FillArgs& a, const PairDesc& pd, 
       break;
     }
     w.b = rl & 31;
-    w.q = s - 32 * tk;
-    const int qmin = slo > 32 * tk ? slo - 32 * tk : 0;
-    switch (t & 3) {
-      case 0: walk_rl<0>(tw, w, qmin, kcap, outv, ops, lane); break;
-      case 1: walk_rl<1>(tw, w, qmin, kcap, outv, ops, lane); break;
-      case 2: walk_rl<2>(tw, w, qmin, kcap, outv, ops, lane); break;
-      default: walk_rl<3>(tw, w, qmin, kcap, outv, ops, lane); break;
+    w.q = s - 64 * cur.u;
+    const int qmin = slo > 64 * cur.u ? slo - 64 * cur.u : 0;
+    const int h = (rl >> 5) & 1, part = w.q >> 6;
+    const int qlo = qmin > 64 * part ? qmin : 64 * part;
+    switch (2 * h + part) {
+      case 0: walk_rl<0, 0>(tw, w, qlo, kcap, outv, ops, lane); break;
+      case 1: walk_rl<0, 1>(tw, w, qlo, kcap, outv, ops, lane); break;
+      case 2: walk_rl<1, 0>(tw, w, qlo, kcap, outv, ops, lane); break;
+      default: walk_rl<1, 1>(tw, w, qlo, kcap, outv, ops, lane); break;
     }
   }
   const bool bad = !out && w.i > 0 && w.j > 0;  // more moves than m + n: inconsistent words
   if (bad && lane == 0) atomicOr(a.err, 16u);
-  if (w.k & 3) outv = lane == ((w.k >> 2) & 63) ? w.acc : outv;
   if ((w.k & 255) && lane < (((w.k & 255) + 3) >> 2)) ops[(int64_t)(w.k >> 8) * 64 + lane] = outv;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a.stamps && lane == 0) {  // trace cycles, tile-wait cycles, moves, switches / demand loads
+    u64* x = a.stamps + 8 * pd.slot;
+    x[2] = __builtin_amdgcn_s_memtime() - c0;
+    x[3] = c_wait;
+    x[4] = (u64)w.k;
+    x[5] = (n_sw << 32) | n_dem;
+  }
   if (lane == 0) {
     a.oplen[pd.slot] = out ? 0 : w.k;
     a.endij[pd.slot] = out ? make_int2(pd.m, pd.n) : make_int2(w.i, w.j);
@@ -226,6 +321,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
   const int wid = threadIdx.x >> 6;
   unsigned* cons = cons_all[wid];
   unsigned* ring = ring_all[wid];
+  // verbose >= 2 timeline (FillArgs::stamps, layout in nwk_runtime.cpp)
+  if (a.stamps && threadIdx.x == 0) atomicMin(a.stamps + 11 * a.ntasks_pairs, (u64)__builtin_amdgcn_s_memrealtime());
   for (;;) {
     unsigned tk = 0;
     if (lane == 0) tk = atomicAdd(a.counter, 1u);
@@ -233,6 +330,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
     if (tk >= (unsigned)a.ntasks) return;
     // wave-uniform exit (a per-lane load would make the task loop divergent)
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load((gu32*)a.err, BITS_RLX)) != 0u) return;
+    const u64 t_task = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+    u64 cyc_wait = 0;
     const int2 task = a.tasks[tk];
     const PairDesc pd = a.pairs[task.x];
     const int band = task.y;
@@ -287,7 +386,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
           w = lane < GO ? h0 : (lane < NV ? 0u : ~0u);
         } else if (j <= kmax) {
           if (!__all(!gl || (unsigned)(g >> 32) == a.epoch)) {
+            const u64 tw = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
             g = gran_wait<kPl>(gin + (int64_t)j * kPs + lane, a.epoch, g, a.err);
+            if (a.stamps) cyc_wait += __builtin_amdgcn_s_memtime() - tw;
             if (!__all(!gl || (unsigned)(g >> 32) == a.epoch)) {
               ok = false;
               break;
@@ -410,6 +511,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
       }
     }
     if (!ok) return;
+    if (a.stamps && lane == 0) {  // per pair: band cycles, of which waiting on the band above
+      atomicAdd(a.stamps + 8 * pd.slot + 6, (u64)(__builtin_amdgcn_s_memtime() - t_task));
+      atomicAdd(a.stamps + 8 * pd.slot + 7, cyc_wait);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -421,12 +526,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // the walk is one latency-bound wave: let it issue ahead of the SIMD's fill waves
       __builtin_amdgcn_s_setprio(3);
+      if (a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
       if (!a.dbg_notrace) {
         trace_gotoh(a, pd, lane);
       } else if (lane == 0) {
         a.oplen[pd.slot] = 0;
         a.endij[pd.slot] = make_int2(pd.m, pd.n);
       }
+      if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
       __builtin_amdgcn_s_setprio(0);
     }
   }
