@@ -164,7 +164,7 @@ def test_no_device_fails_loudly(lib):
         seqalign.getMinimumPenalties([b"AC", b"CA"], 2, 3, 2, [0])
 
 
-@pytest.mark.parametrize("field,value", [("kernel", 7), ("kernel", -1), ("finalize", 4), ("bits", 5), ("task_order", 3),
+@pytest.mark.parametrize("field,value", [("kernel", 8), ("kernel", -1), ("finalize", 4), ("bits", 5), ("task_order", 3),
                                          ("task_order", -1)])
 def test_ctx_create_rejects_bad_options(lib, field, value):
     """nwk_ctx_create checks its options before looking for a device: a bad
