@@ -58,6 +58,7 @@ METRIC = "DP cell-updates/s (GCUPS) on k-way SoP MSA; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 SIMDS = 1024                   # 256 CUs x 4 SIMDs
 VALU_CYC_PER_WAVE_INSTR = 2    # MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles
+SPEC_CLOCK_HZ = 2.4e9          # MI355X_MICROARCH.md: peak engine clock (the spec-clock roofline)
 BYTES_PER_CELL = 4.0           # the reference's int32 matrix (sub:428, 478-487)
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
@@ -246,9 +247,14 @@ def roofline(workload, kernel, launch_s, my_cells, launches):
     clk = pmc["grbm_gui_active_per_launch"] / 8.0 / (pmc["duration_ns_per_launch"] * 1e-9)  # Hz, 8 XCDs
     insts = pmc["sq_insts_valu_per_launch"]
     valu_frac = insts * VALU_CYC_PER_WAVE_INSTR / SIMDS / (clk * launch_s)
+    # (the guide's peak clock: frac_spec_clock prices the same issue against 2.4 GHz,
+    # "frac" against the clock the counters measured -- both reported)
+    valu_frac_spec = insts * VALU_CYC_PER_WAVE_INSTR / SIMDS / (SPEC_CLOCK_HZ * launch_s)
     valu = {"achieved": round(insts * 64 / launch_s / 1e12, 2),
             "peak": round(SIMDS * 64 / VALU_CYC_PER_WAVE_INSTR * clk / 1e12, 2),
             "unit": "Tlane-op/s", "frac": round(valu_frac, 4), "clock_GHz": round(clk / 1e9, 3),
+            "peak_spec_clock": round(SIMDS * 64 / VALU_CYC_PER_WAVE_INSTR * SPEC_CLOCK_HZ / 1e12, 2),
+            "frac_spec_clock": round(valu_frac_spec, 4), "spec_clock_GHz": SPEC_CLOCK_HZ / 1e9,
             "valu_wave_instr_per_launch": insts}
     traffic = pmc["hbm_bytes_per_launch"]
     hbm = {"achieved": round(traffic / launch_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -256,7 +262,9 @@ def roofline(workload, kernel, launch_s, my_cells, launches):
     bound = "valu" if valu["frac"] >= hbm["frac"] else "hbm"
     top = valu if bound == "valu" else hbm
     out.update({"bound": bound, "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"],
-                "frac": top["frac"], "traffic": traffic, "valu": valu, "hbm": hbm,
+                "frac": top["frac"], "frac_clock": "measured" if bound == "valu" else None,
+                "frac_spec_clock": valu["frac_spec_clock"] if bound == "valu" else top["frac"],
+                "traffic": traffic, "valu": valu, "hbm": hbm,
                 "counters_from": pmc["_file"] + " (rocprofv3 --pmc passes of this bench command; "
                                  "duration measured live here, counters per launch from the passes)"})
     return out
