@@ -121,6 +121,27 @@ def cpu_share():
     return max(share, 1), hi
 
 
+def _run_beating(cmd, data, timeout, tag):
+    """subprocess.run(cmd, input=data) that prints a heartbeat to stderr every 30 s
+    (a GPU-box command silent for 3 minutes is taken to be hung)."""
+    import threading
+
+    p = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    res = {}
+    th = threading.Thread(target=lambda: res.update(zip(("out", "err"), p.communicate(data))))
+    th.start()
+    t0 = time.perf_counter()
+    while th.is_alive():
+        th.join(30)
+        if th.is_alive():
+            if time.perf_counter() - t0 > timeout:
+                p.kill()
+                th.join()
+                raise subprocess.TimeoutExpired(cmd, timeout)
+            print("%s: running %.0f s" % (tag, time.perf_counter() - t0), file=sys.stderr, flush=True)
+    return subprocess.CompletedProcess(cmd, p.returncode, res.get("out", b""), res.get("err", b""))
+
+
 def cpu_baseline(genes, pxy, pgap, affine=None, budget_s=60.0, expect_pen=None, expect_hs=None):
     """The CPU path on a bounded prefix subset of the workload (>= 60 s, the
     depth BASELINE.md §3 asks for: "the first P' pairs in canonical order, with
@@ -179,7 +200,7 @@ def cpu_baseline(genes, pxy, pgap, affine=None, budget_s=60.0, expect_pen=None, 
                 want = (seqalign.chain_hash(np.asarray(expect_hs)[:Pk]), [int(v) for v in expect_pen[:Pk]])
             runs = []
             for attempt in range(2):
-                r = subprocess.run(cmd, input=text, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=900)
+                r = _run_beating(cmd, text, 900, "cpu_baseline (reference sub, attempt %d)" % (attempt + 1))
                 if r.returncode != 0:
                     raise RuntimeError("exit %d: %s" % (r.returncode, r.stderr[-300:].decode("latin-1")))
                 lines = r.stdout.decode("latin-1").split("\n")
