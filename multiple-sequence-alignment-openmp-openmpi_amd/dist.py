@@ -399,6 +399,10 @@ class NodeRecords:
             except FileNotFoundError:
                 pass
             self.shm = shared_memory.SharedMemory(name=self.name, create=True, size=size)
+            # flags cleared BEFORE the nonce goes out: a peer may publish as soon
+            # as it has it (clearing after the collective erased a fast peer's
+            # first flag, and rank 0 waited for it forever)
+            np.ndarray((self.world, chunks), dtype=np.int64, buffer=self.shm.buf, offset=64)[:] = 0
             nonce = int.from_bytes(os.urandom(6), "little") | 1
             np.ndarray((1,), dtype=np.int64, buffer=self.shm.buf)[0] = nonce
         nonce = int(comm.max(float(nonce)))  # rank 0's nonce (< 2^53), after it created the segment
@@ -409,8 +413,6 @@ class NodeRecords:
         self.flags = np.ndarray((self.world, chunks), dtype=np.int64, buffer=self.shm.buf, offset=64)
         self.data = np.ndarray((self.world, self.sum_per, REC), dtype=np.uint8, buffer=self.shm.buf,
                                offset=self.data_off)
-        if self.rank == 0:
-            self.flags[:] = 0
 
     def publish(self, c, block, token):
         """This rank's padded block of piece c, then its flag."""
