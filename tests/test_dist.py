@@ -465,3 +465,45 @@ def test_node_records_stale_segment_is_replaced():
         nr.close()
     finally:
         stale.close()
+
+
+def test_node_records_fast_peer_flag_survives():
+    """NodeRecords: a peer may publish as soon as rank 0's nonce collective
+    returns to it, before rank 0's own constructor has finished -- its flag
+    must survive (rank 0 used to clear the flags after the collective, erasing
+    such a flag, and then waited for it forever).  Two ranks in one process:
+    rank 0's max() runs rank 1's whole attach + publish."""
+    import sys
+
+    sys.path.insert(0, PKG)
+    import dist as nwdist
+
+    key = "f%d" % os.getpid()
+    blk = nwdist.pack_records([1, 2], [5, 6], np.full((2, 64), 3, dtype=np.uint8), 2)
+    peer = {}
+
+    class Peer:
+        world, rank = 2, 1
+
+        def __init__(self, nonce):
+            self.nonce = nonce
+
+        def max(self, x):
+            return float(self.nonce)
+
+    class Root:
+        world, rank = 2, 0
+
+        def max(self, x):  # the collective: the fast peer attaches and publishes piece 0 now
+            peer["nr"] = nwdist.NodeRecords(Peer(int(x)), 1, [2], key=key)
+            peer["nr"].publish(0, blk, 1)
+            return x
+
+    nr = nwdist.NodeRecords(Root(), 1, [2], key=key)
+    try:
+        nr.publish(0, blk, 1)
+        got = nr.wait(0, 1, timeout_s=2)
+        assert got.shape[0] == 4 and (got[2:] == blk).all()
+    finally:
+        peer["nr"].close()
+        nr.close()
