@@ -53,12 +53,9 @@ struct GGeo {
 
 // At least NWK_GOTOH_WPE waves per SIMD: the step is issue-bound and a lone
 // wave issues a VALU op only every ~8 cycles, so occupancy is
-// what fills the SIMD, and a band waiting on the band above (~35% of band
-// time on C5) leaves its slot to the others.  5 waves (96 VGPRs; the C5
-// instance spills 45 VGPRs, outside the step loop) ran C5 at 6716 GCUPS
-// against 6633 at 4 (128 VGPRs, no spills).
+// what fills the SIMD; the probe's step needed 104-117 VGPRs (4 waves fit).
 #ifndef NWK_GOTOH_WPE
-#define NWK_GOTOH_WPE 5
+#define NWK_GOTOH_WPE 4
 #endif
 
 // Waits until lanes 0 .. kPl - 1 hold granules tagged `epoch` (v: their last
