@@ -54,20 +54,23 @@ __device__ __forceinline__ unsigned col_addc(unsigned a, unsigned b, u64& c) {
 }
 
 // The carries' hop to the next lane, on the scalar unit (written out so the
-// compiler keeps it there): lane 63's carry out of the previous step (bit 63)
-// enters the band's last-row shift register acc, then c = (c << 1) | the band
-// above's bit QQ of this half (lane 0's carry in).
+// compiler keeps it there): c = (c << 1) | the band above's bit QQ of this half
+// (lane 0's carry in), and lane 63's carry out of the previous step (bit 63 of
+// the old c) enters the band's last-row shift register acc.  One SCC chain, 4
+// SALU: SCC = inj bit QQ; lo = 2 lo + SCC (SCC = old bit 31); hi = 2 hi + SCC
+// (SCC = old bit 63); acc = 2 acc + SCC.  (Was 5: a 64-bit shift, a bit
+// extract and an OR for c, a bit test and an add for acc.)
 template <int QQ>
 __device__ __forceinline__ void col_hop(u64& c, unsigned& acc, u64 inj) {
-  u64 t;
-  asm("s_bitcmp1_b64 %[c], 63\n\t"
-      "s_addc_u32 %[acc], %[acc], %[acc]\n\t"
-      "s_lshl_b64 %[c], %[c], 1\n\t"
-      "s_bfe_u64 %[t], %[inj], %[pos]\n\t"
-      "s_or_b64 %[c], %[c], %[t]"
-      : [c] "+s"(c), [acc] "+s"(acc), [t] "=&s"(t)
-      : [inj] "s"(inj), [pos] "i"(QQ | (1 << 16))
+  unsigned lo = (unsigned)c, hi = (unsigned)(c >> 32);
+  asm("s_bitcmp1_b64 %[inj], %[pos]\n\t"
+      "s_addc_u32 %[lo], %[lo], %[lo]\n\t"
+      "s_addc_u32 %[hi], %[hi], %[hi]\n\t"
+      "s_addc_u32 %[acc], %[acc], %[acc]"
+      : [lo] "+s"(lo), [hi] "+s"(hi), [acc] "+s"(acc)
+      : [inj] "s"(inj), [pos] "i"(QQ)
       : "scc");
+  c = ((u64)hi << 32) | lo;
 }
 
 // G_K's middle terms OR_{d = D .. I-1} (~l_d & T_{K+d})
