@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # C5 A/B: gotoh band issue priority (NWK_BAND_PRIO=1) vs off, alternating, same box.
 set -uo pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 mkdir -p gpurun_out/c5prio
 for rep in 1 2; do
   for v in 0 1; do

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # same-box A/B of the column kernel's hop order: base (tree) vs NWK_LIB=tools/varlib/hopfwd.so, alternating.
 set -uo pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 mkdir -p gpurun_out/colab2
 for rep in 1 2; do
   for v in base fwd; do

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # col hop change: column-kernel parity, then the C3 / C4 bench lines, then the shard emulations.
 set -uo pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../../.."
 mkdir -p gpurun_out/colhop
 timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_col.py tests/test_gpu_shard.py > gpurun_out/colhop/tests.txt 2>&1 || { tail -20 gpurun_out/colhop/tests.txt; exit 1; }
 tail -1 gpurun_out/colhop/tests.txt

@@ -1,6 +1,6 @@
 """Repeat test_affine_packed_windowed_storage_and_full_rerun[40]'s job and report wrong pairs."""
 import json, os, random, sys
-REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 sys.path.insert(0, os.path.join(REPO, "multiple-sequence-alignment-openmp-openmpi_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
