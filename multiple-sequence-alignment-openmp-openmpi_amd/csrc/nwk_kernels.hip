@@ -1537,6 +1537,9 @@ __device__ __forceinline__ void wait_vm_keep4(unsigned& a, unsigned& b, u64& c, 
 // a scalar three-state machine over v_readlane.  Moves are emitted reversed:
 // 'D', 'U'/'L' (gap extended) and 'u'/'l' (the gap's first column: the host
 // charges go + ge there, ge for the others).
+// LIN: every code is a fresh move (nw_profile's linear gaps set both "opened"
+// bits), so the walk needs no gap state: a cell's two low bits are its move.
+template <bool LIN = false>
 __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairDesc& pd, TbLds<4>& L, int lane, unsigned* prog) {
   using C = TbConf<4>;
   constexpr int SPD = C::SPC;
@@ -1610,8 +1613,23 @@ __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairD
     if (prog && lane == 0) __hip_atomic_store((gu32*)prog, 0x51000000u | (code & 0xff) << 8 | (nit & 0xff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // scalar walk through the block
     int di = 0, dj = 0;
+    const int li_lim = min(i, 8), lj_lim = min(j, 8);  // (LIN) leave the block or reach row / column 0
     for (;;) {
       const unsigned c = __builtin_amdgcn_readlane(code, di * 8 + dj);
+      if constexpr (LIN) {
+        const unsigned src = c & 3u;
+        if (src == 3u) {
+          bad = true;  // not a code the fill writes
+          break;
+        }
+        const unsigned op = (0x6c7544u >> (8 * src)) & 0xffu;  // 'D', 'u', 'l'
+        di += (3u >> src) & 1u;
+        dj += (5u >> src) & 1u;
+        asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(op) : "memory");
+        ++Lc;
+        if (di >= li_lim || dj >= lj_lim) break;
+        continue;
+      }
       unsigned op;
       op = 0;
       if (st == 0) {
@@ -2273,14 +2291,39 @@ __global__ __launch_bounds__(256) NWK_PKA_OCC void nw_align_pka(FillArgs a) {
 // set (a linear gap is always a fresh gap), so trace_pair_affine walks it
 // unchanged: 'D', 'u' (X column vs a gap column), 'l' (gap column vs Y).
 // ===========================================================================
+// DOT: how the row / column profiles' six counts are packed (host: nwk_msa,
+// per launch): 4 = u8 x 4 in ints 0-1 (v_dot4_u32_u8), 2 = u16 x 2 in ints
+// 0-2 (v_dot2_u32_u16), 0 = one int each (v_mad_u32_u24); the packed forms
+// repeat a column's gy right after the counts, so a step reads one 16-byte
+// entry.  H is carried as the key 4H (+ the move in bits 0-1 while a cell is
+// decided): the three candidates are 4 d, 4 u + 1, 4 l + 2, so one v_min3_u32 gives the cell's
+// value and its move with the D < U < L tie order of trace_pair_affine's
+// codes, and key | 12 is the stored 4-bit code.  The DP stays below 2^30
+// (nwk_msa's admission check), so 4H + 3 fits a u32.
+template <int DOT, int N>
+__device__ __forceinline__ unsigned prof_sub(const unsigned (&rp)[N], const int4& c0) {
+  if constexpr (DOT == 4) {
+    return __builtin_amdgcn_udot4(rp[1], (unsigned)c0.y, __builtin_amdgcn_udot4(rp[0], (unsigned)c0.x, 0u, false), false);
+  } else if constexpr (DOT == 2) {
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    unsigned t = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, rp[0]), __builtin_bit_cast(us2, (unsigned)c0.x), 0u, false);
+    t = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, rp[1]), __builtin_bit_cast(us2, (unsigned)c0.y), t, false);
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(us2, rp[2]), __builtin_bit_cast(us2, (unsigned)c0.z), t, false);
+  } else {
+    return 0u;  // (the unpacked form reads both int4s: prof_sub6)
+  }
+}
+
+template <int DOT>
 __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
   constexpr int W = 4, SPD = 8;
-  __shared__ __attribute__((aligned(16))) int ring_all[4][128];
+  constexpr int NP = DOT == 4 ? 2 : DOT == 2 ? 3 : 6;  // packed ints per profile entry
+  __shared__ __attribute__((aligned(16))) unsigned ring_all[4][128];
   __shared__ __attribute__((aligned(16))) int4 cwin_all[4][2][256];  // 128 columns x 8 ints, two slots
   __shared__ __attribute__((aligned(16))) TbLds<W> tbl[4];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  int* ring = ring_all[wid];
+  unsigned* ring = ring_all[wid];
   unsigned* prog = a.prog ? a.prog + blockIdx.x * 4 + wid : nullptr;
 
   for (;;) {
@@ -2294,20 +2337,22 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
     const PairDesc pd = a.pairs[task.x];
     const int band = task.y;
     const int row0 = band * kBandRows + lane * kRows;  // 0-based first DP row of this lane
-    int rc[kRows][kProfSyms], gx[kRows], h[kRows];
-    unsigned acc[kRows];
+    unsigned rp[kRows][NP], gxk[kRows], h[kRows], acc[kRows];
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
       const int row = min(row0 + r, pd.m - 1);  // rows past m: copies of the last (never traced)
       const int4* pr = reinterpret_cast<const int4*>(a.prow + (pd.x_off + row) * 8);
       const int4 q0 = pr[0], q1 = pr[1];
-      rc[r][0] = q0.x; rc[r][1] = q0.y; rc[r][2] = q0.z; rc[r][3] = q0.w; rc[r][4] = q1.x; rc[r][5] = q1.y;
-      gx[r] = q1.z;
-      h[r] = q1.w;  // H[i][0]
+      const unsigned e[8] = {(unsigned)q0.x, (unsigned)q0.y, (unsigned)q0.z, (unsigned)q0.w,
+                             (unsigned)q1.x, (unsigned)q1.y, (unsigned)q1.z, (unsigned)q1.w};
+#pragma unroll
+      for (int b = 0; b < NP; ++b) rp[r][b] = e[b];
+      gxk[r] = 4u * e[6] + 1u;  // up move key increment
+      h[r] = 4u * e[7];         // H[i][0]
       acc[r] = 0;
     }
-    int Up = band == 0 ? 0 : a.prow[(pd.x_off + band * kBandRows - 1) * 8 + 7];  // H[row above the band][0]
-    int stH = 0;
+    unsigned Up = band == 0 ? 0u : 4u * (unsigned)a.prow[(pd.x_off + band * kBandRows - 1) * 8 + 7];  // H[row above the band][0]
+    unsigned stH = 0;
     const bool from_above = band > 0;
     const bool to_below = band + 1 < pd.nbands;
     const int64_t bstride = (int64_t)pd.nchunks * 64;
@@ -2324,61 +2369,59 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
     u64 pend = from_above ? ld_granule(gin) : 0;
     bool ok = true;
 
-    for (int sb = 0; sb < pd.sblocks; ++sb) {
-      int bval;  // band-above row: H[row above][64sb + 1 + lane]
-      if (from_above) {
-        bval = 0;
-        if (sb < pd.nchunks) {
-          if (!__all((unsigned)(pend >> 32) == a.epoch)) pend = wait_granules(gin + 64 * sb, a.epoch, pend, a.err);
-          if (!__all((unsigned)(pend >> 32) == a.epoch)) { ok = false; break; }
-          bval = (int)(unsigned)pend;
-        }
-        pend = ld_granule(gin + 64 * min(sb + 1, last_chunk));  // next chunk, used at the next super-block
-      } else {
-        bval = a.pcol[(pd.y_off + 64 * sb + lane + 1) * 8 + 7];  // H[0][j]
-      }
-      int* slot = ring + (sb & 1) * 64;
-      slot[lane] = bval;
-      int4* cw = cwin_all[wid][sb & 1];
-      // columns 64sb-63 .. 64sb+64: 128 entries of 8 ints = 256 int4
-#pragma unroll
-      for (int k = 0; k < 4; ++k) cw[lane + 64 * k] = colg[128 * sb + lane + 64 * k];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
+    // one super-block of 64 steps; MASK: super-block 0, whose first 63 steps
+    // reach lanes before their column 1 (the border H[i][0] stays)
+    auto run_sb = [&](int sb, auto maskc) {
+      constexpr bool MASK = decltype(maskc)::value;
+      const unsigned* slot = ring + (sb & 1) * 64;
+      const int4* cw = cwin_all[wid][sb & 1];
+      // column entries are read one step ahead (the LDS latency hides behind a step)
+      auto ld_col = [&](int we, int4& x0, int4& x1) {
+        x0 = cw[2 * we];
+        if constexpr (DOT == 0) x1 = cw[2 * we + 1];
+      };
+      int4 n0, n1 = make_int4(0, 0, 0, 0);
+      ld_col(64 - lane, n0, n1);
       for (int blk = 0; blk < 8; ++blk) {
         const int s0 = sb * 64 + blk * 8;
-        const int4 bA = *reinterpret_cast<const int4*>(slot + blk * 8);
-        const int4 bB = *reinterpret_cast<const int4*>(slot + blk * 8 + 4);
-        const int bv[8] = {bA.x, bA.y, bA.z, bA.w, bB.x, bB.y, bB.z, bB.w};
+        const uint4 bA = *reinterpret_cast<const uint4*>(slot + blk * 8);
+        const uint4 bB = *reinterpret_cast<const uint4*>(slot + blk * 8 + 4);
+        const unsigned bv[8] = {bA.x, bA.y, bA.z, bA.w, bB.x, bB.y, bB.z, bB.w};
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           stH = __builtin_amdgcn_update_dpp(h[kRows - 1], stH, 0x130 /*wave_shl:1*/, 0xf, 0xf, false);
-          const int uh = __builtin_amdgcn_update_dpp(bv[k], h[kRows - 1], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
-          const int dg0 = Up;
+          const unsigned uh = __builtin_amdgcn_update_dpp(bv[k], h[kRows - 1], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
+          const unsigned dg0 = Up;
           Up = uh;
           // this lane's column j = s - lane + 1 -> window entry j - (64sb - 63) = (s - 64sb) - lane + 64
           const int we = blk * 8 + k - lane + 64;
-          const int4 c0 = cw[2 * we], c1 = cw[2 * we + 1];
-          const int cy[kProfSyms] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y};
-          const int gy = c1.z;
-          const bool valid = (s0 + k) >= lane;  // column >= 1; else the border H[i][0] stays
-          int nh[kRows], hp = uh;
+          const int4 c0 = n0, c1 = n1;
+          if (k < 7 || blk < 7) ld_col(we + 1, n0, n1);
+          // left move key increment: gy follows the packed counts (int 2 / 3), or int 6
+          const unsigned lk = 4u * (unsigned)(DOT == 4 ? c0.z : DOT == 2 ? c0.w : c1.z) + 2u;
+          const bool valid = !MASK || (s0 + k) >= lane;
+          unsigned hp = uh, nh[kRows];
 #pragma unroll
           for (int r = 0; r < kRows; ++r) {
-            int sub = 0;
+            unsigned sub;
+            if constexpr (DOT == 0) {
+              const unsigned cy[kProfSyms] = {(unsigned)c0.x, (unsigned)c0.y, (unsigned)c0.z,
+                                              (unsigned)c0.w, (unsigned)c1.x, (unsigned)c1.y};
+              sub = 0;
 #pragma unroll
-            for (int b = 0; b < kProfSyms; ++b) sub += (int)__umul24((unsigned)rc[r][b], (unsigned)cy[b]);
-            const int d = (r ? h[r - 1] : dg0) + sub;  // diag: row above, previous step
-            const int u = hp + gx[r];                   // up: row above, this step
-            const int l = h[r] + gy;                    // left: this row, previous step
-            const int hv = min(min(d, u), l);
-            const unsigned code = (d == hv ? 0u : (u == hv ? 1u : 2u)) | 12u;
-            acc[r] = __builtin_amdgcn_alignbit(code, acc[r], 4);
-            nh[r] = valid ? hv : h[r];
+              for (int b = 0; b < kProfSyms; ++b) sub += __umul24(rp[r][b], cy[b]);
+            } else {
+              sub = prof_sub<DOT>(rp[r], c0);
+            }
+            const unsigned d = (r ? h[r - 1] : dg0) + 4u * sub;  // diag: row above, previous step
+            const unsigned key = min(min(d, h[r] + lk), hp + gxk[r]);
+            acc[r] = __builtin_amdgcn_alignbit(key | 12u, acc[r], 4);
+            const unsigned nv = key & ~3u;
+            nh[r] = MASK ? (valid ? nv : h[r]) : nv;
             hp = nh[r];
           }
 #pragma unroll
-          for (int r = 0; r < kRows; ++r) h[r] = nh[r];
+          for (int r = 0; r < kRows; ++r) h[r] = nh[r];  // (d above read the previous step's h[r - 1])
           if (k == 7) {
 #pragma unroll
             for (int r = 0; r < kRows; ++r) __builtin_nontemporal_store(acc[r], mptr + r * kWave);
@@ -2387,7 +2430,33 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
         }
         mptr += (8 / SPD) * kRows * kWave;
       }
-      if (to_below && sb >= 1 && sb <= pd.nchunks) st_granule(gout + 64 * (sb - 1), a.epoch, stH);
+    };
+
+    for (int sb = 0; sb < pd.sblocks; ++sb) {
+      unsigned bval;  // band-above row: H[row above][64sb + 1 + lane] (key form 4H)
+      if (from_above) {
+        bval = 0;
+        if (sb < pd.nchunks) {
+          if (!__all((unsigned)(pend >> 32) == a.epoch)) pend = wait_granules(gin + 64 * sb, a.epoch, pend, a.err);
+          if (!__all((unsigned)(pend >> 32) == a.epoch)) { ok = false; break; }
+          bval = (unsigned)pend;
+        }
+        pend = ld_granule(gin + 64 * min(sb + 1, last_chunk));  // next chunk, used at the next super-block
+      } else {
+        bval = 4u * (unsigned)a.pcol[(pd.y_off + 64 * sb + lane + 1) * 8 + 7];  // H[0][j]
+      }
+      ring[(sb & 1) * 64 + lane] = bval;
+      int4* cw = cwin_all[wid][sb & 1];
+      // columns 64sb-63 .. 64sb+64: 128 entries of 8 ints = 256 int4
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cw[lane + 64 * k] = colg[128 * sb + lane + 64 * k];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (sb == 0)
+        run_sb(sb, std::true_type{});
+      else
+        run_sb(sb, std::false_type{});
+      if (to_below && sb >= 1 && sb <= pd.nchunks) st_granule(gout + 64 * (sb - 1), a.epoch, (int)stH);
       __builtin_amdgcn_wave_barrier();
       PROG(0x20000000u | ((unsigned)band << 12) | (unsigned)(sb & 0xfff));
     }
@@ -2403,7 +2472,10 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       PROG(0x40000000u);
-      trace_pair_affine(a, pd, tbl[wid], lane, prog);
+      // nwk_msa verbose >= 2: {walk start, walk end} per merge (s_memrealtime, 100 MHz)
+      if (a.stamps && lane == 0) a.stamps[2 * pd.slot] = __builtin_amdgcn_s_memrealtime();
+      trace_pair_affine<true>(a, pd, tbl[wid], lane, prog);
+      if (a.stamps && lane == 0) a.stamps[2 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
       PROG(0x60000000u);
     }
   }
@@ -2443,7 +2515,14 @@ hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStrea
       return hipGetLastError();
     case kProfileDP:
       if (bits != 4) return hipErrorInvalidValue;
-      hipLaunchKernelGGL(nw_profile, dim3(grid), dim3(256), 0, s, a);
+      if (a.prof_dot == 4)
+        hipLaunchKernelGGL(nw_profile<4>, dim3(grid), dim3(256), 0, s, a);
+      else if (a.prof_dot == 2)
+        hipLaunchKernelGGL(nw_profile<2>, dim3(grid), dim3(256), 0, s, a);
+      else if (a.prof_dot == 0)
+        hipLaunchKernelGGL(nw_profile<0>, dim3(grid), dim3(256), 0, s, a);
+      else
+        return hipErrorInvalidValue;
       return hipGetLastError();
     case kAffinePk:
       if (bits != 4) return hipErrorInvalidValue;
@@ -2472,7 +2551,7 @@ int fill_blocks_per_cu(int mode, int bits) {
                     : mode == kAffinePk ? reinterpret_cast<const void*>(&nw_align_pka)
                     : mode == kPacked   ? reinterpret_cast<const void*>(&nw_align_pk)
                     : mode == kPacked2  ? reinterpret_cast<const void*>(&nw_align_pk2)
-                                        : reinterpret_cast<const void*>(&nw_profile);
+                                        : reinterpret_cast<const void*>(&nw_profile<0>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 256, 0) != hipSuccess) return 1;
     return n > 0 ? n : 1;
   }

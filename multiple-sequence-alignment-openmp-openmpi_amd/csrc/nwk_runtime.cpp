@@ -2803,9 +2803,10 @@ int nwk_device_synchronize(int32_t device) {
 namespace {
 
 struct Prof {
-  std::vector<uint8_t> rows;  // nseq x len, row-major ('_' = gap)
+  std::vector<int> cnt;       // len x S column counts (S - 1 = gaps); freed once merged
+  std::vector<int> up;        // column -> column of the merged profile (set by the merge)
   std::vector<int> members;   // input sequence index of each row
-  int len = 0;
+  int len = 0, parent = -1;
 };
 
 inline int64_t sym_cost(int a, int b, int gap, int pxy, int pgap) {
@@ -2814,14 +2815,10 @@ inline int64_t sym_cost(int a, int b, int gap, int pxy, int pgap) {
 }
 
 // Column symbol counts of a profile (S symbols, the last = gap).
-void prof_counts(const Prof& P, const uint8_t* code_of, int S, std::vector<int>* cnt) {
-  const int n = (int)P.members.size();
-  cnt->assign((size_t)P.len * S, 0);
-  for (int r = 0; r < n; ++r)
-    for (int i = 0; i < P.len; ++i) {
-      const uint8_t ch = P.rows[(size_t)r * P.len + i];
-      (*cnt)[(size_t)i * S + (ch == '_' ? S - 1 : code_of[ch])]++;
-    }
+// a leaf's column counts (merged profiles add their children's along the path)
+void leaf_counts(const uint8_t* seq, int len, const uint8_t* code_of, int S, std::vector<int>* cnt) {
+  cnt->assign((size_t)len * S, 0);
+  for (int i = 0; i < len; ++i) (*cnt)[(size_t)i * S + code_of[seq[i]]]++;
 }
 
 // NWK_WATCHDOG=<s> debug: report the wave markers of a launch that does not finish, then exit.
@@ -2856,12 +2853,19 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
   if (S > kProfSyms) return fail(NWK_EINVAL, "nwk_msa: %d distinct input bytes (at most %d)", c->alpha, kProfSyms - 1);
   *len = 0;
   *sop = 0;
+  // stats (nwk_last_stats): fill_ms = the nw_profile launches (HIP events), traceback_ms = 0 (the
+  // walk runs inside them), cells = sum of merge DP cells, fill_launches = batches = tree levels
+  const double t_start = now_ms();
+  nwk_stats st{};
+  st.mode = kProfileDP;
+  st.bits = 4;
+  c->stats = st;
   if (k == 0) return NWK_OK;
   const int nc = 2 * k - 1;
   std::vector<Prof> prof((size_t)nc);
   for (int s = 0; s < k; ++s) {
     prof[s].len = (int)(c->off[s + 1] - c->off[s]);
-    prof[s].rows.assign(c->seqs.begin() + c->off[s], c->seqs.begin() + c->off[s + 1]);
+    leaf_counts(c->seqs.data() + c->off[s], prof[s].len, c->code_of, S, &prof[s].cnt);
     prof[s].members = {s};
   }
   // ---- UPGMA (oracle nwo_msa): mean pairwise penalty, exact ratio compare, ties -> smallest ids
@@ -2897,6 +2901,7 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
   int rc;
   const int max_round = k > 1 ? round_of[nc - 1] : 0;
   DevBuf &d_prow = c->d_msa[0], &d_pcol = c->d_msa[1], &d_mw = c->d_msa[2], &d_pd = c->d_pairs, &d_tk = c->d_tasks;
+  double t_lvl = now_ms(), t_prep = 0, t_wait = 0;  // (verbose >= 2: host phases per level)
   for (int rd = 1; rd <= max_round; ++rd) {
     std::vector<Merge> ms;
     for (const auto& m : merges)
@@ -2905,15 +2910,15 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
     // ---- profile arrays: X columns (DP rows) {rc[0..5], gx, H[i][0]}, Y columns {cnt[0..5], gy, H[0][j]}
     std::vector<int> hrow, hcol;
     std::vector<PairDesc> pd((size_t)np);
-    std::vector<std::vector<int>> cy_host((size_t)np), rc_host((size_t)np);
-    int64_t mat = 0, bnd = 0, ops = 0, ntasks = 0;
+    std::vector<std::vector<int>> rc_host((size_t)np);
+    int64_t mat = 0, bnd = 0, ops = 0, ntasks = 0, maxpk = 0;  // maxpk: largest rc / count (profile packing)
     for (int q = 0; q < np; ++q) {
       const Prof &X = prof[ms[q].x], &Y = prof[ms[q].y];
       const int nx = (int)X.members.size(), ny = (int)Y.members.size(), LX = X.len, LY = Y.len;
-      std::vector<int> cx, cyv;
-      prof_counts(X, c->code_of, S, &cx);
-      prof_counts(Y, c->code_of, S, &cyv);
+      const std::vector<int>& cx = X.cnt;
+      const std::vector<int>& cyv = Y.cnt;
       int64_t maxstep = 0, acc = 0;
+      maxpk = std::max<int64_t>(maxpk, std::max(nx, ny));  // (a column count is at most its profile's members)
       const int64_t xoff = (int64_t)hrow.size() / 8;
       std::vector<int>& rch = rc_host[q];
       rch.assign((size_t)LX * 8, 0);
@@ -2927,7 +2932,7 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
         rch[(size_t)i * 8 + 6] = (int)gx;
         rch[(size_t)i * 8 + 7] = (int)acc;
         int64_t mx = gx;
-        for (int b = 0; b < S; ++b) mx = std::max(mx, rcb[b] * ny);
+        for (int b = 0; b < S; ++b) mx = std::max(mx, rcb[b] * ny), maxpk = std::max(maxpk, rcb[b]);
         maxstep = std::max(maxstep, mx);
         if (mx >= (1 << 24)) return fail(NWK_EINVAL, "nwk_msa: profile costs exceed the kernel's 24-bit products");
       }
@@ -2946,7 +2951,7 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
         maxstep = std::max(maxstep, gy);
       }
       for (int j = LY + 1; j < LY + 192; ++j) colv[(size_t)(64 + j) * 8 + 7] = (int)accy;  // (never traced)
-      cy_host[q] = cyv;
+
       hcol.insert(hcol.end(), colv.begin(), colv.end());
       if ((int64_t)(LX + LY + 2) * maxstep + acc + accy >= (1ll << 30))
         return fail(NWK_EINVAL, "nwk_msa: profile DP of %d x %d columns would exceed int32", LX, LY);
@@ -2967,6 +2972,25 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       bnd += (int64_t)d.nbands * d.nchunks * 64;  // granules of each band's last row (the last band's unused)
       ops += round_up((int64_t)LX + LY, 16);
       ntasks += d.nbands;
+      st.cells += (double)LX * LY;
+      st.matrix_bytes += 4 * (int64_t)d.nbands * band_dwords(4, d.sblocks);
+    }
+    // ---- pack ints 0-5 of every profile entry for nw_profile<DOT> (rc_host / Prof::cnt keep the plain counts)
+    int dot = maxpk < 256 ? 4 : maxpk < 65536 ? 2 : 0;
+    if (const char* ev = getenv("NWK_PROF_DOT")) dot = std::min(dot, atoi(ev) >= 4 ? 4 : atoi(ev) >= 2 ? 2 : 0);  // (A/B)
+    if (dot) {
+      for (std::vector<int>* v : {&hrow, &hcol}) {
+        for (size_t e = 0; e < v->size(); e += 8) {
+          int* p = v->data() + e;
+          uint32_t w[3] = {0, 0, 0};
+          for (int b = 0; b < kProfSyms; ++b) {
+            if (dot == 4) w[b >> 2] |= (uint32_t)p[b] << (8 * (b & 3));
+            else w[b >> 1] |= (uint32_t)p[b] << (16 * (b & 1));
+          }
+          for (int b = 0; b < kProfSyms; ++b) p[b] = b < 3 ? (int)w[b] : 0;
+          p[dot == 4 ? 2 : 3] = p[6];  // gy (gx) next to the counts: one 16-byte LDS read per column step
+        }
+      }
     }
     // ---- device buffers: [granules | matrices | ops]
     const int64_t bnd_b = round_up(bnd * 8 + 4096, 256), mat_b = round_up(mat * 4, 256);
@@ -3007,6 +3031,7 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
     fa.ntasks_pairs = np;
     fa.prow = d_prow.as<int>();
     fa.pcol = d_pcol.as<int>();
+    fa.prof_dot = dot;
     const int grid = (int)std::min<int64_t>(fill_blocks_per_cu(kProfileDP, 4) * c->cus, ceil_div(ntasks, 4));
     if (getenv("NWK_WATCHDOG")) {
       if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;
@@ -3017,7 +3042,15 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       fprintf(stderr, "nwk_msa round %d: %d merges, %lld band tasks, grid %d\n", rd, np, (long long)ntasks, grid);
       fflush(stderr);
     }
+    if (c->opts.verbose >= 2) {
+      if ((rc = c->d_stamps.ensure(16 * (size_t)np)) != NWK_OK) return rc;
+      HIP_TRY(hipMemsetAsync(c->d_stamps.p, 0, 16 * (size_t)np, c->stream));
+      fa.stamps = c->d_stamps.as<unsigned long long>();
+    }
+    t_prep = now_ms();
+    HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(launch_fill(kProfileDP, 4, fa, grid, c->stream));
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     watchdog_wait(c, fa.prog, grid);
     std::vector<int> ol((size_t)np);
     std::vector<int2> ej((size_t)np);
@@ -3029,6 +3062,25 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
     HIP_TRY(hipMemcpyAsync(hops.data(), d_mw.as<uint8_t>() + bnd_b + mat_b, (size_t)ops, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (herr) return fail(NWK_EKERNEL, "nwk_msa: profile kernel fault (err=%u)", herr);
+    t_wait = now_ms();
+    float lvl_ms = 0;
+    HIP_TRY(hipEventElapsedTime(&lvl_ms, c->ev[0], c->ev[1]));
+    st.fill_ms += lvl_ms;
+    ++st.fill_launches;
+    ++st.batches;
+    if (c->opts.verbose >= 2) {
+      std::vector<unsigned long long> sw((size_t)2 * np);
+      HIP_TRY(hipMemcpy(sw.data(), fa.stamps, 16 * (size_t)np, hipMemcpyDeviceToHost));
+      double wmax = 0, wsum = 0;
+      for (int q = 0; q < np; ++q) {
+        const double w = sw[2 * q + 1] > sw[2 * q] ? (sw[2 * q + 1] - sw[2 * q]) * 1e-5 : 0.0;  // 100 MHz ticks -> ms
+        wmax = std::max(wmax, w);
+        wsum += w;
+      }
+      fprintf(stderr, "nwk_msa level %d: %d merges, %lld band tasks, %.3f ms (walks: longest %.3f ms, sum %.3f ms); host: "
+              "previous merges + profiles %.3f ms, launch to results %.3f ms\n", rd, np,
+              (long long)ntasks, (double)lvl_ms, wmax, wsum, t_prep - t_lvl, t_wait - t_prep);
+    }
     // ---- merged profiles and merge costs (forward moves: prefix run, then the reversed trace)
     for (int q = 0; q < np; ++q) {
       const Prof &X = prof[ms[q].x], &Y = prof[ms[q].y];
@@ -3045,17 +3097,32 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       N.len = (int)mv.size();
       N.members = X.members;
       N.members.insert(N.members.end(), Y.members.begin(), Y.members.end());
-      N.rows.assign((size_t)(nx + ny) * N.len, '_');
+      N.cnt.assign((size_t)N.len * S, 0);
+      Prof &Xm = prof[ms[q].x], &Ym = prof[ms[q].y];
+      Xm.up.assign((size_t)X.len, 0);
+      Ym.up.assign((size_t)Y.len, 0);
+      Xm.parent = Ym.parent = ms[q].id;
       int64_t cost = 0;
       int i = 0, j = 0;
       const std::vector<int>& rch = rc_host[q];
-      const std::vector<int>& cyv = cy_host[q];
+      const std::vector<int>& cyv = Y.cnt;
       for (int t = 0; t < N.len; ++t) {
         const char m = mv[(size_t)t];
         if ((m != 'L' && i >= X.len) || (m != 'U' && j >= Y.len))
           return fail(NWK_EKERNEL, "nwk_msa: traced path leaves the %d x %d matrix", X.len, Y.len);
-        if (m != 'L') for (int r = 0; r < nx; ++r) N.rows[(size_t)r * N.len + t] = X.rows[(size_t)r * X.len + i];
-        if (m != 'U') for (int r = 0; r < ny; ++r) N.rows[(size_t)(nx + r) * N.len + t] = Y.rows[(size_t)r * Y.len + j];
+        int* nc_t = &N.cnt[(size_t)t * S];
+        if (m != 'L') {
+          for (int b = 0; b < S; ++b) nc_t[b] += X.cnt[(size_t)i * S + b];
+          Xm.up[(size_t)i] = t;
+        } else {
+          nc_t[gap] += nx;
+        }
+        if (m != 'U') {
+          for (int b = 0; b < S; ++b) nc_t[b] += cyv[(size_t)j * S + b];
+          Ym.up[(size_t)j] = t;
+        } else {
+          nc_t[gap] += ny;
+        }
         if (m == 'D') {
           for (int b = 0; b < S; ++b) cost += (int64_t)rch[(size_t)i * 8 + b] * cyv[(size_t)j * S + b];
         } else if (m == 'U') {
@@ -3068,15 +3135,35 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       }
       if (i != X.len || j != Y.len) return fail(NWK_EKERNEL, "nwk_msa: traced path ends at (%d, %d) of (%d, %d)", i, j, X.len, Y.len);
       *sop += cost;
-      prof[ms[q].x] = Prof();
-      prof[ms[q].y] = Prof();
+      std::vector<int>().swap(Xm.cnt);
+      std::vector<int>().swap(Ym.cnt);
     }
+    t_lvl = t_wait;
   }
+  st.total_ms = now_ms() - t_start;
+  c->stats = st;
+  if (c->opts.verbose)
+    fprintf(stderr, "nwk_msa: k %d, %d levels, %.3g cells, fill %.3f ms (%.1f GCUPS), total %.3f ms\n", k, st.fill_launches,
+            st.cells, st.fill_ms, st.fill_ms > 0 ? st.cells / st.fill_ms / 1e6 : 0.0, st.total_ms);
   const Prof& R = prof[nc - 1];
   if (R.len > cap) return fail(NWK_EINVAL, "nwk_msa: MSA length %d exceeds cap %lld", R.len, (long long)cap);
   *len = R.len;
-  for (size_t r = 0; r < R.members.size(); ++r)
-    memcpy(rows + (size_t)R.members[r] * cap, R.rows.data() + r * R.len, (size_t)R.len);
+  // rows, top down: a node's column -> MSA column (parents have larger ids than their children)
+  std::vector<std::vector<int>> pos((size_t)nc);
+  pos[nc - 1].resize((size_t)R.len);
+  for (int t = 0; t < R.len; ++t) pos[nc - 1][(size_t)t] = t;
+  for (int v = nc - 2; v >= 0; --v) {
+    const Prof& P = prof[v];
+    const std::vector<int>& pp = pos[(size_t)P.parent];
+    pos[(size_t)v].resize((size_t)P.len);
+    for (int t = 0; t < P.len; ++t) pos[(size_t)v][(size_t)t] = pp[(size_t)P.up[(size_t)t]];
+    if (v >= k) continue;
+    uint8_t* row = rows + (size_t)v * cap;
+    memset(row, '_', (size_t)R.len);
+    const uint8_t* sq = c->seqs.data() + c->off[v];
+    for (int t = 0; t < P.len; ++t) row[pos[(size_t)v][(size_t)t]] = sq[t];
+  }
+  if (k == 1) memcpy(rows, c->seqs.data() + c->off[0], (size_t)R.len);
   return NWK_OK;
 }
 
