@@ -162,7 +162,6 @@ struct FillArgs {
   int ntjobs;              // jobs the batch will produce
   const int* prow;         // kProfileDP: per X column (DP row) 8 ints {rc[0..5], gx, H[i][0]} at pairs[].x_off
   const int* pcol;         // kProfileDP: per Y column (DP column) 8 ints {cnt[0..5], gy, H[0][j]} at pairs[].y_off
-  int prof_dot;            // kProfileDP: rc / cnt packing of ints 0-5 (4: u8 x 4, 2: u16 x 2, 0: one each; nw_profile<DOT>)
   const unsigned* yw;      // kBits: per y position p two dwords (code bit planes of y[p .. p+31], y[p] at bit 31), at pairs[].e_off
   int* retry;              // windowed storage: per slot, 1 = the path left the stored window (re-run in full)
   int strip_ring;          // kBitsStrip: LDS dwords per wave of the hand-off ring (max n' / 64 x 2 NP)

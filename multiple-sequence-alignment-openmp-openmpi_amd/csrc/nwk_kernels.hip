@@ -2515,11 +2515,12 @@ hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStrea
       return hipGetLastError();
     case kProfileDP:
       if (bits != 4) return hipErrorInvalidValue;
-      if (a.prof_dot == 4)
+      // (kProfileDP passes the profile packing in lin_mode, which only nw_align reads)
+      if (a.lin_mode == 4)
         hipLaunchKernelGGL(nw_profile<4>, dim3(grid), dim3(256), 0, s, a);
-      else if (a.prof_dot == 2)
+      else if (a.lin_mode == 2)
         hipLaunchKernelGGL(nw_profile<2>, dim3(grid), dim3(256), 0, s, a);
-      else if (a.prof_dot == 0)
+      else if (a.lin_mode == 0)
         hipLaunchKernelGGL(nw_profile<0>, dim3(grid), dim3(256), 0, s, a);
       else
         return hipErrorInvalidValue;

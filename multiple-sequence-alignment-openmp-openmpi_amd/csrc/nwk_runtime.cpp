@@ -3031,7 +3031,7 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
     fa.ntasks_pairs = np;
     fa.prow = d_prow.as<int>();
     fa.pcol = d_pcol.as<int>();
-    fa.prof_dot = dot;
+    fa.lin_mode = dot;  // the profile packing: nw_profile<4 | 2 | 0> (launch_fill)
     const int grid = (int)std::min<int64_t>(fill_blocks_per_cu(kProfileDP, 4) * c->cus, ceil_div(ntasks, 4));
     if (getenv("NWK_WATCHDOG")) {
       if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;

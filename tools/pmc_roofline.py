@@ -72,10 +72,12 @@ if out["sq_insts_valu_per_launch"] and out["grbm_gui_active_per_launch"]:
     out["valu_issue_frac"] = out["sq_insts_valu_per_launch"] * 2 / 1024 / cyc
     out["clock_ghz"] = cyc / out["duration_ns_per_launch"]
     out["hbm_frac_at_pmc_duration"] = out.get("hbm_bytes_per_launch", 0) / (out["duration_ns_per_launch"] * 1e-9) / 8e12
-out["method"] = ("rocprofv3 --kernel-trace --pmc in three separate passes over 'bench.py --workload %s "
-                 "--steps 1 --warmup 1 --no-cpu-baseline' (tools/gpu_round.sh); per-launch means over the "
+# PMC_CMD: the profiled command when it is not bench.py (e.g. profiles/r05/scripts/msa_prof.sh)
+cmd = os.environ.get("PMC_CMD") or ("'bench.py --workload %s --steps 1 --warmup 1 --no-cpu-baseline' "
+                                    "(tools/gpu_round.sh)" % wl)
+out["method"] = ("rocprofv3 --kernel-trace --pmc in three separate passes over %s; per-launch means over the "
                  "kernel's dispatches; traffic = (2 x FETCH_SIZE + WRITE_SIZE) KiB; valu_issue_frac = "
-                 "SQ_INSTS_VALU x 2 / 1024 / (GRBM_GUI_ACTIVE / 8)" % wl)
+                 "SQ_INSTS_VALU x 2 / 1024 / (GRBM_GUI_ACTIVE / 8)" % cmd)
 dst = os.path.join(REPO, "profiles", rnd, "pmc_%s%s.json" % (wl, suffix))
 os.makedirs(os.path.dirname(dst), exist_ok=True)
 json.dump(out, open(dst, "w"), indent=1)
