@@ -163,7 +163,9 @@ int nwk_align_pairs_poll(nwk_ctx *ctx, int64_t from, int32_t *penalties, uint8_t
 int nwk_align_all(nwk_ctx *ctx, int32_t pxy, int32_t pgap, int32_t *penalties,
                   uint8_t *problem_hash, char *hash_hex);
 
-/* Statistics of the context's last nwk_align_pairs call. */
+/* Statistics of the context's last nwk_align_pairs call, or of its last nwk_msa call
+ * (fill_ms = the nw_profile launches incl. their walks, cells = the merges' DP cells,
+ * fill_launches = batches = guide-tree levels, mode 6, traceback_ms 0). */
 int nwk_last_stats(const nwk_ctx *ctx, nwk_stats *out);
 
 /*
