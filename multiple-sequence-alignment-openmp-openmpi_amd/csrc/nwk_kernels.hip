@@ -2293,7 +2293,9 @@ __global__ __launch_bounds__(256) NWK_PKA_OCC void nw_align_pka(FillArgs a) {
 // ===========================================================================
 // DOT: how the row / column profiles' six counts are packed (host: nwk_msa,
 // per launch): 4 = u8 x 4 in ints 0-1 (v_dot4_u32_u8), 2 = u16 x 2 in ints
-// 0-2 (v_dot2_u32_u16), 0 = one int each (v_mad_u32_u24); the packed forms
+// 0-2 (v_dot2_u32_u16), 0 = one int each (v_mad_u32_u24); 5 = rows as 4 with
+// single-sequence columns, whose count is one-hot: int 0 is the v_perm
+// selector of the column's symbol (one v_perm per cell); the packed forms
 // repeat a column's gy right after the counts, so a step reads one 16-byte
 // entry.  H is carried as the key 4H (+ the move in bits 0-1 while a cell is
 // decided): the three candidates are 4 d, 4 u + 1, 4 l + 2, so one v_min3_u32 gives the cell's
@@ -2302,7 +2304,9 @@ __global__ __launch_bounds__(256) NWK_PKA_OCC void nw_align_pka(FillArgs a) {
 // (nwk_msa's admission check), so 4H + 3 fits a u32.
 template <int DOT, int N>
 __device__ __forceinline__ unsigned prof_sub(const unsigned (&rp)[N], const int4& c0) {
-  if constexpr (DOT == 4) {
+  if constexpr (DOT == 5) {
+    return __builtin_amdgcn_perm(rp[1], rp[0], (unsigned)c0.x);  // one-hot column: rc[its symbol]
+  } else if constexpr (DOT == 4) {
     return __builtin_amdgcn_udot4(rp[1], (unsigned)c0.y, __builtin_amdgcn_udot4(rp[0], (unsigned)c0.x, 0u, false), false);
   } else if constexpr (DOT == 2) {
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -2317,7 +2321,7 @@ __device__ __forceinline__ unsigned prof_sub(const unsigned (&rp)[N], const int4
 template <int DOT>
 __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
   constexpr int W = 4, SPD = 8;
-  constexpr int NP = DOT == 4 ? 2 : DOT == 2 ? 3 : 6;  // packed ints per profile entry
+  constexpr int NP = DOT >= 4 ? 2 : DOT == 2 ? 3 : 6;  // packed ints per profile entry
   __shared__ __attribute__((aligned(16))) unsigned ring_all[4][128];
   __shared__ __attribute__((aligned(16))) int4 cwin_all[4][2][256];  // 128 columns x 8 ints, two slots
   __shared__ __attribute__((aligned(16))) TbLds<W> tbl[4];
@@ -2398,7 +2402,7 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
           const int4 c0 = n0, c1 = n1;
           if (k < 7 || blk < 7) ld_col(we + 1, n0, n1);
           // left move key increment: gy follows the packed counts (int 2 / 3), or int 6
-          const unsigned lk = 4u * (unsigned)(DOT == 4 ? c0.z : DOT == 2 ? c0.w : c1.z) + 2u;
+          const unsigned lk = 4u * (unsigned)(DOT >= 4 ? c0.z : DOT == 2 ? c0.w : c1.z) + 2u;
           const bool valid = !MASK || (s0 + k) >= lane;
           unsigned hp = uh, nh[kRows];
 #pragma unroll
@@ -2516,7 +2520,9 @@ hipError_t launch_fill(int mode, int bits, const FillArgs& a, int grid, hipStrea
     case kProfileDP:
       if (bits != 4) return hipErrorInvalidValue;
       // (kProfileDP passes the profile packing in lin_mode, which only nw_align reads)
-      if (a.lin_mode == 4)
+      if (a.lin_mode == 5)
+        hipLaunchKernelGGL(nw_profile<5>, dim3(grid), dim3(256), 0, s, a);
+      else if (a.lin_mode == 4)
         hipLaunchKernelGGL(nw_profile<4>, dim3(grid), dim3(256), 0, s, a);
       else if (a.lin_mode == 2)
         hipLaunchKernelGGL(nw_profile<2>, dim3(grid), dim3(256), 0, s, a);

@@ -2976,19 +2976,36 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       st.matrix_bytes += 4 * (int64_t)d.nbands * band_dwords(4, d.sblocks);
     }
     // ---- pack ints 0-5 of every profile entry for nw_profile<DOT> (rc_host / Prof::cnt keep the plain counts)
-    int dot = maxpk < 256 ? 4 : maxpk < 65536 ? 2 : 0;
-    if (const char* ev = getenv("NWK_PROF_DOT")) dot = std::min(dot, atoi(ev) >= 4 ? 4 : atoi(ev) >= 2 ? 2 : 0);  // (A/B)
+    // 5: every merge's columns are one sequence (a caterpillar guide tree's levels), so a
+    // column's counts are one-hot and a cell's substitution cost is a byte select
+    bool one_hot = true;
+    for (int q = 0; q < np; ++q) one_hot = one_hot && prof[ms[q].y].members.size() == 1;
+    int dot = maxpk < 256 ? (one_hot ? 5 : 4) : maxpk < 65536 ? 2 : 0;
+    if (const char* ev = getenv("NWK_PROF_DOT")) {  // (A/B: caps the form)
+      const int cap = atoi(ev);
+      dot = std::min(dot, cap >= 5 ? 5 : cap >= 4 ? 4 : cap >= 2 ? 2 : 0);
+      if (dot == 5 && !one_hot) dot = 4;
+    }
     if (dot) {
       for (std::vector<int>* v : {&hrow, &hcol}) {
         for (size_t e = 0; e < v->size(); e += 8) {
           int* p = v->data() + e;
+          if (dot == 5 && v == &hcol) {  // selector of the one symbol counted (none: bytes 0x0c = zero)
+            uint32_t sel = 0x0c0c0c0cu;
+            for (int b = 0; b < kProfSyms; ++b)
+              if (p[b]) sel = 0x0c0c0c00u | (uint32_t)b;
+            for (int b = 0; b < kProfSyms; ++b) p[b] = 0;
+            p[0] = (int)sel;
+            p[2] = p[6];
+            continue;
+          }
           uint32_t w[3] = {0, 0, 0};
           for (int b = 0; b < kProfSyms; ++b) {
-            if (dot == 4) w[b >> 2] |= (uint32_t)p[b] << (8 * (b & 3));
+            if (dot >= 4) w[b >> 2] |= (uint32_t)p[b] << (8 * (b & 3));
             else w[b >> 1] |= (uint32_t)p[b] << (16 * (b & 1));
           }
           for (int b = 0; b < kProfSyms; ++b) p[b] = b < 3 ? (int)w[b] : 0;
-          p[dot == 4 ? 2 : 3] = p[6];  // gy (gx) next to the counts: one 16-byte LDS read per column step
+          p[dot >= 4 ? 2 : 3] = p[6];  // gy (gx) next to the counts: one 16-byte LDS read per column step
         }
       }
     }
@@ -3031,7 +3048,7 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
     fa.ntasks_pairs = np;
     fa.prow = d_prow.as<int>();
     fa.pcol = d_pcol.as<int>();
-    fa.lin_mode = dot;  // the profile packing: nw_profile<4 | 2 | 0> (launch_fill)
+    fa.lin_mode = dot;  // the profile packing: nw_profile<5 | 4 | 2 | 0> (launch_fill)
     const int grid = (int)std::min<int64_t>(fill_blocks_per_cu(kProfileDP, 4) * c->cus, ceil_div(ntasks, 4));
     if (getenv("NWK_WATCHDOG")) {
       if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;

@@ -721,12 +721,14 @@ def test_msa_random_vs_oracle(engine, seed):
     assert oracle.sop(rows, pxy, pgap) == s
 
 
-@pytest.mark.parametrize("pxy,pgap,force", [(3, 2, "4"), (3, 2, "2"), (3, 2, "0"), (150, 90, None), (40000, 30000, None)],
-                         ids=["dot4", "dot2-forced", "mad-forced", "dot2-natural", "mad-natural"])
+@pytest.mark.parametrize("pxy,pgap,force", [(3, 2, None), (3, 2, "4"), (3, 2, "2"), (3, 2, "0"), (150, 90, None),
+                                            (40000, 30000, None)],
+                         ids=["auto", "dot4-forced", "dot2-forced", "mad-forced", "dot2-natural", "mad-natural"])
 def test_msa_profile_packings(engine, monkeypatch, pxy, pgap, force):
-    """nw_profile<DOT>: the u8 x 4 (v_dot4), u16 x 2 (v_dot2) and plain (v_mad_u24) profile forms
-    give the oracle's MSA.  Large costs pick the wider forms by themselves (rc = members x cost
-    >= 256, >= 65536); NWK_PROF_DOT caps the form on small costs."""
+    """nw_profile<DOT>: the one-hot (v_perm: levels whose columns are single sequences), u8 x 4
+    (v_dot4), u16 x 2 (v_dot2) and plain (v_mad_u24) profile forms give the oracle's MSA.  Large
+    costs pick the wider forms by themselves (rc = members x cost >= 256, >= 65536);
+    NWK_PROF_DOT caps the form on small costs."""
     if force is not None:
         monkeypatch.setenv("NWK_PROF_DOT", force)
     r = random.Random(900 + pxy)
