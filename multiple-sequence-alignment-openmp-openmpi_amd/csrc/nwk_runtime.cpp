@@ -2900,6 +2900,9 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
   HIP_TRY(hipSetDevice(c->device));
   int rc;
   const int max_round = k > 1 ? round_of[nc - 1] : 0;
+  int64_t cst[kProfSyms][kProfSyms];  // symbol pair costs (gap = S - 1)
+  for (int a2 = 0; a2 < S; ++a2)
+    for (int b = 0; b < S; ++b) cst[a2][b] = sym_cost(a2, b, gap, pxy, pgap);
   DevBuf &d_prow = c->d_msa[0], &d_pcol = c->d_msa[1], &d_mw = c->d_msa[2], &d_pd = c->d_pairs, &d_tk = c->d_tasks;
   double t_lvl = now_ms(), t_prep = 0, t_wait = 0;  // (verbose >= 2: host phases per level)
   for (int rd = 1; rd <= max_round; ++rd) {
@@ -2924,8 +2927,11 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       rch.assign((size_t)LX * 8, 0);
       for (int i = 0; i < LX; ++i) {
         int64_t rcb[kProfSyms] = {0};
-        for (int b = 0; b < S; ++b)
-          for (int a2 = 0; a2 < S; ++a2) rcb[b] += (int64_t)cx[(size_t)i * S + a2] * sym_cost(a2, b, gap, pxy, pgap);
+        for (int a2 = 0; a2 < S; ++a2) {
+          const int64_t na = cx[(size_t)i * S + a2];
+          if (na)
+            for (int b = 0; b < S; ++b) rcb[b] += na * cst[a2][b];
+        }
         const int64_t gx = (int64_t)(nx - cx[(size_t)i * S + gap]) * ny * pgap;
         acc += gx;
         for (int b = 0; b < kProfSyms; ++b) rch[(size_t)i * 8 + b] = (int)(b < S ? rcb[b] : 0);
