@@ -2904,7 +2904,7 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
   for (int a2 = 0; a2 < S; ++a2)
     for (int b = 0; b < S; ++b) cst[a2][b] = sym_cost(a2, b, gap, pxy, pgap);
   DevBuf &d_prow = c->d_msa[0], &d_pcol = c->d_msa[1], &d_mw = c->d_msa[2], &d_pd = c->d_pairs, &d_tk = c->d_tasks;
-  double t_lvl = now_ms(), t_prep = 0, t_wait = 0;  // (verbose >= 2: host phases per level)
+  double t_lvl = now_ms(), t_prep = 0, t_wait = 0, t_build = 0;  // (verbose >= 2: host phases per level)
   for (int rd = 1; rd <= max_round; ++rd) {
     std::vector<Merge> ms;
     for (const auto& m : merges)
@@ -3016,6 +3016,7 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       }
     }
     // ---- device buffers: [granules | matrices | ops]
+    t_build = now_ms();
     const int64_t bnd_b = round_up(bnd * 8 + 4096, 256), mat_b = round_up(mat * 4, 256);
     const int64_t work_b = bnd_b + mat_b + ops + 4096;
     if ((rc = d_mw.ensure((size_t)work_b)) != NWK_OK) return rc;
@@ -3101,8 +3102,8 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
         wsum += w;
       }
       fprintf(stderr, "nwk_msa level %d: %d merges, %lld band tasks, %.3f ms (walks: longest %.3f ms, sum %.3f ms); host: "
-              "previous merges + profiles %.3f ms, launch to results %.3f ms\n", rd, np,
-              (long long)ntasks, (double)lvl_ms, wmax, wsum, t_prep - t_lvl, t_wait - t_prep);
+              "previous merges + profiles %.3f ms, uploads %.3f ms, launch to results %.3f ms\n", rd, np,
+              (long long)ntasks, (double)lvl_ms, wmax, wsum, t_build - t_lvl, t_prep - t_build, t_wait - t_prep);
     }
     // ---- merged profiles and merge costs (forward moves: prefix run, then the reversed trace)
     for (int q = 0; q < np; ++q) {
