@@ -1614,7 +1614,24 @@ __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairD
     // scalar walk through the block
     int di = 0, dj = 0;
     const int li_lim = min(i, 8), lj_lim = min(j, 8);  // (LIN) leave the block or reach row / column 0
-    for (;;) {
+    // (LIN, pd.prio != 0: nwk_msa's merges of few sequences, whose paths seldom leave the
+    // diagonal) diagonal runs: when every cell from the block's entry to its edge along the
+    // diagonal is a D, the r moves go out at once (one lane-masked LDS write)
+    const bool diag_try = LIN && pd.prio != 0;
+    const u64 dmask = diag_try ? __ballot((code & 3u) == 0u) : 0ull;
+    auto diag_run = [&]() -> bool {
+      const int r = min(li_lim - di, lj_lim - dj);  // >= 1 inside the block
+      const u64 d8 = 0x8040201008040201ull;
+      const u64 m = (r >= 8 ? d8 : d8 & ((1ull << (9 * r - 8)) - 1ull)) << (di * 8 + dj);
+      if ((dmask & m) != m) return false;
+      if (lane < r) asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((Lc + lane) & 255)), "v"((unsigned)'D') : "memory");
+      Lc += r;
+      di += r;
+      dj += r;
+      return true;
+    };
+    if (diag_try && diag_run()) {
+    } else for (;;) {
       const unsigned c = __builtin_amdgcn_readlane(code, di * 8 + dj);
       if constexpr (LIN) {
         const unsigned src = c & 3u;

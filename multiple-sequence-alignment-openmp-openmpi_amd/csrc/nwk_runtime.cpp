@@ -2971,6 +2971,10 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       d.nchunks = (int)ceil_div(LY, 64);
       d.sblocks = d.nchunks + 1;
       d.slot = q;
+      // the walk's diagonal-run fast path (trace_pair_affine<true>): merges of <= 16
+      // sequences (k8 x 50k: 133 -> 140 e2e GCUPS; k64 / k256's wide profiles, whose
+      // paths turn often, run slower with it)
+      d.prio = nx + ny <= 16 ? 1 : 0;
       d.mat_off = mat;
       d.bnd_off = bnd;
       d.ops_off = ops;
