@@ -2,6 +2,9 @@
 # nw_profile A/B: the committed library (tools/varlib/libnwk_head.so, built from
 # the previous commit) against the in-tree build, then the in-tree build's
 # forced profile forms and a kernel trace.  Output under gpurun_out/msa/.
+# The baseline library (not kept): git archive 1b9d9fe multiple-sequence-alignment-openmp-openmpi_amd include
+# | tar -x -C /tmp/old && make -C /tmp/old/multiple-sequence-alignment-openmp-openmpi_amd, then copy its
+# lib/libnwk.so to tools/varlib/libnwk_head.so.
 set -e
 cd "$(dirname "$0")/../../.."
 mkdir -p gpurun_out/msa
