@@ -740,6 +740,20 @@ def test_msa_profile_packings(engine, monkeypatch, pxy, pgap, force):
     assert oracle.sop(rows, pxy, pgap) == s
 
 
+def test_msa_many_sequences_vs_oracle(engine):
+    """20 mutants of one 2,000-base sequence: a deep guide tree whose levels cross every
+    nw_profile form in one call -- one-hot leaf columns (v_perm), multi-member columns
+    (v_dot4), the walk's diagonal runs (merges of <= 16 sequences) and the plain walk
+    (wider merges); bit-exact against the oracle's MSA and SoP."""
+    r = random.Random(2024)
+    genes = _mutants(r, bytes(r.choice(ACGT) for _ in range(2000)), 20, ACGT)
+    engine.set_sequences(genes)
+    rows, s = engine.msa(3, 2)
+    st = engine.stats()
+    assert st["fill_launches"] >= 5, st
+    assert (rows, s) == oracle.msa(genes, 3, 2)
+
+
 def test_msa_small_and_edge_sets(engine):
     for genes in ([b"ACGT"], [b"A", b"A"], [b"A", b"C"], [b"AC", b"A", b"C", b"CA"], [b"A" * 600, b"C"]):
         engine.set_sequences(genes)
