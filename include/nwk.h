@@ -102,6 +102,8 @@ typedef struct nwk_stats {
   int32_t linear_space_pairs; /* pairs aligned with the linear-space traceback */
   int32_t window_retries;    /* windowed storage: pairs re-run wider (path left the window) */
   int32_t window;            /* storage window W in columns of the call's first pairs (0 = full storage) */
+  int32_t guard_checked;     /* pairs whose walked path's cost was checked against the fill's own dp[m][n] */
+  int32_t guard_reruns;      /* pairs re-run because their walked path's cost differed from it (skel:274) */
 } nwk_stats;
 
 /* Defaults for nwk_opts (device 0, auto everything). */

@@ -59,11 +59,14 @@ namespace {
 //            entering column 0 of its next pass sees the left border)
 //   sto      the block is inside the pair's stored blocks (uniform); lsto: this
 //            lane's words hold a cell of the storage window (bits_lane_stored)
-template <int NP, int SR, bool MASK, bool PROD>
+//   END      steps that may hold column capc = n - 1: the bit there (row 32 lane
+//            + s - capc - 32 lane) adds its vertical difference to cnt when its
+//            row is < m (rowm) -- the fill-vs-walk guard's end value, FillArgs::endv
+template <int NP, int SR, bool MASK, bool PROD, bool END = false>
 __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsigned x1, unsigned yp0, unsigned yp1,
                                            unsigned w0, unsigned w1, unsigned (&H)[NP], unsigned (&V)[NP],
                                            const unsigned* cons, unsigned* ring, unsigned* st, bool sto, int eh,
-                                           bool lsto) {
+                                           bool lsto, int capc = 0, unsigned rowm = 0, int* cnt = nullptr) {
   unsigned dw[8], uw[8];
   // the band-above entries are read one step ahead (an LDS read's latency
   // would otherwise sit on every step's dependence chain)
@@ -143,6 +146,12 @@ __device__ __forceinline__ void bits_block(int s0, int lane, unsigned x0, unsign
       const unsigned M = e >= 31 ? ~0u : (e < 0 ? 0u : (2u << e) - 1u);
 #pragma unroll
       for (int k = 0; k < NP; ++k) V[k] &= M;
+    }
+    if constexpr (END) {
+      const int bb = s - capc - 32 * lane;
+      const unsigned mk = (unsigned)bb < 32u ? (1u << bb) & rowm : 0u;
+#pragma unroll
+      for (int k = 0; k < NP; ++k) *cnt += __builtin_popcount(V[k] & mk);
     }
     if constexpr (PROD) {  // lane 63 bit 31 = the band's last row at column s - 2047
       if (lane == 63) {
@@ -647,6 +656,18 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
     bool ok = true;
     const u64 t_task = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
     u64 cyc_wait = 0, cyc_wait0 = 0, n_wait = 0;
+    // fill-vs-walk guard: G(m, n) = -sum of v down column n; row 32 t + b
+    // reaches column n - 1 (0-based) at step n - 1 + 32 t + b: super-blocks sbe ..
+    const int capc = pd.n - 1;
+    const bool want_end = a.endv != nullptr;
+    const int sbe = want_end ? capc >> 6 : nsb;
+    const int capx = want_end ? capc : -100000;
+    int cnt = 0;
+    unsigned rowm;
+    {
+      const int nvr = pd.m - R0 - 32 * lane;
+      rowm = nvr >= 32 ? ~0u : (nvr <= 0 ? 0u : (1u << nvr) - 1u);
+    }
 
     for (int sb = 0; sb < nsb; ++sb) {
       BITS_PROG(0x20000000u | (unsigned)sb);
@@ -699,9 +720,20 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
         const int eh = s0 - 32 * lane;
         bool ls = true;
         if (lwin) ls = bits_lane_stored(hi0 + (int64_t)s0 * pd.m, lim, hlim);
-        if (mask) {
-          if (prod) bits_block<NP, SR, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls);
-          else bits_block<NP, SR, true, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls);
+        if (mask) {  // (the masked super-blocks always take the guard's END form)
+          if (prod)
+            bits_block<NP, SR, true, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls,
+                                                 capx, rowm, &cnt);
+          else
+            bits_block<NP, SR, true, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls,
+                                                  capx, rowm, &cnt);
+        } else if (sb >= sbe) {
+          if (prod)
+            bits_block<NP, SR, false, true, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls,
+                                                  capx, rowm, &cnt);
+          else
+            bits_block<NP, SR, false, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh,
+                                                   ls, capx, rowm, &cnt);
         } else {
           if (prod) bits_block<NP, SR, false, true>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls);
           else bits_block<NP, SR, false, false>(s0, lane, x0, x1, yp0, yp1, w0, w1, H, V, cons, rblk, st, sto, eh, ls);
@@ -730,6 +762,13 @@ __global__ __launch_bounds__(256) NWK_BITS_OCC void nw_align_bits(FillArgs a) {
     }
     BITS_PROG(0x30000000u);
     if (!ok) return;
+    if (want_end) {  // this band's part of H(m, n): - sum v (+ (m + n) pgap once, band 0)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+      if (lane == 0)
+        __hip_atomic_fetch_add((gu32*)(a.endv + pd.slot), (unsigned)(band == 0 ? (pd.m + pd.n) * a.pgap - cnt : -cnt),
+                               BITS_RLX);
+    }
     if (a.stamps && lane == 0) {  // per pair: band cycles, of which waiting on the band above
       atomicAdd(a.stamps + 8 * pd.slot + 6, (u64)(__builtin_amdgcn_s_memtime() - t_task));
       atomicAdd(a.stamps + 8 * pd.slot + 7, cyc_wait);

@@ -204,9 +204,19 @@ __device__ __forceinline__ bool fin_rows(const FillArgs& a, const PairDesc& pd, 
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) pen += __shfl_xor(pen, o);
+  pen += pre * a.pgap;
   if (lane == 0) {
     a.fin_len[pd.slot] = pre + nops;  // both rows have this length
-    a.fin_len[a.ntasks_pairs + pd.slot] = pen + pre * a.pgap;
+    a.fin_len[a.ntasks_pairs + pd.slot] = pen;
+  }
+  // the fill-vs-walk guard (skel:274): the walked path must cost the fill's
+  // H(m, n); a pair that disagrees is not queued (no record) and re-runs
+  if (a.endv && !__any(off)) {
+    const int ev = (int)__hip_atomic_load((gu32*)(a.endv + pd.slot), BITS_RLX);
+    if (__builtin_amdgcn_readfirstlane(pen) != ev) {
+      if (lane == 0) a.retry[pd.slot] = 2;
+      return false;
+    }
   }
   return !__any(off);
 }

@@ -132,10 +132,14 @@ __device__ __forceinline__ void col_hops(u64 (&c)[NP], unsigned (&acc)[NP], cons
 //   inj      the band above's last row for lane 0's columns of this half (bit q = column s_half + q)
 //   pub      CAP: acc after step s_half + 30's carries (columns s_half - 94 .. s_half - 63)
 //   MASK     steps of the first super-block: columns < 0 keep v = 0 (the left border)
-template <int NP, int SR, bool MASK, bool CAP, int BLK>
+//   END      steps that may hold column capc = n - 1: the lane there adds the
+//            vertical differences of its rows (rowm: those < m) to cnt (the
+//            fill-vs-walk guard's end value, FillArgs::endv)
+template <int NP, int SR, bool MASK, bool CAP, int BLK, bool END>
 __device__ __forceinline__ void col_block(int s0, int lane, unsigned x0, unsigned x1, unsigned w0, unsigned w1,
                                           unsigned (&l)[NP], u64 (&c)[NP], unsigned (&acc)[NP],
-                                          const u64 (&inj)[NP], unsigned (&pub)[NP], unsigned* st, bool sto) {
+                                          const u64 (&inj)[NP], unsigned (&pub)[NP], unsigned* st, bool sto,
+                                          int capc, unsigned rowm, int& cnt) {
   unsigned dw[8], uw[8];
   auto step = [&](auto qc) {
     constexpr int q = decltype(qc)::value;
@@ -162,6 +166,11 @@ __device__ __forceinline__ void col_block(int s0, int lane, unsigned x0, unsigne
     }
 #pragma unroll
     for (int k = 0; k < NP; ++k) l[k] = Vn[k];
+    if constexpr (END) {
+      const unsigned mk = s - lane == capc ? rowm : 0u;
+#pragma unroll
+      for (int k = 0; k < NP; ++k) cnt += __builtin_popcount(Vn[k] & mk);
+    }
     if constexpr (SR < 0) dw[q] = match;
     else if constexpr (SR >= NP) dw[q] = ~0u;
     else dw[q] = BOP3(match, D[SR], D[SR], kA | ~kB);  // match | ~D_SR
@@ -444,6 +453,15 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
     flushed = e;
   };
   int b = (pd.m - 1) / kBR, r = (pd.m - 1) % kBR, c = pd.n - 1;
+  if (!SPEC && a.dbg_corrupt == pd.slot + 1) {
+    // (tests of the fill-vs-walk guard) flip the stored D bit of cell (m, n):
+    // lane r / 32 holds it at step c + r / 32, bit r % 32 of the diag word
+    const int s = c + (r >> 5), rel = (s >> 3) - bits_blk_lo(b, pd.m, pd.n, win);
+    if (lane == 0 && (unsigned)rel < (unsigned)nblk)
+      __hip_atomic_fetch_xor((gu32*)(mat + (int64_t)b * bdw + (int64_t)rel * 1024 + ((s & 7) >> 2) * 256 + 4 * (r >> 5) + (s & 3)),
+                             1u << (r & 31), BITS_RLX);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   if constexpr (SPEC) {  // band sb's last row, at the proportional diagonal's column
     b = sb;
     r = kBR - 1;
@@ -930,16 +948,18 @@ __device__ __forceinline__ void trace_col(const FillArgs& a, const PairDesc& pd,
     a.endij[pd.slot] = o_end;
     if (out) a.retry[pd.slot] = 1;
     if (a.host_rec) {
-      int* h = a.host_rec + 4 * pd.slot;
+      int* h = a.host_rec + kHostRecInts * pd.slot;
       h[1] = out ? -1 : bad ? -2 : o_len;  // -1: re-run wider, -2: failed (never finalized)
       h[2] = o_end.x;
       h[3] = o_end.y;
+      h[4] = a.endv ? (int)__hip_atomic_load((gu32*)(a.endv + pd.slot), BITS_RLX) : 0;  // the fill's H(m, n)
     }
   }
   if (a.host_rec) {  // the moves (host memory) and the record, then its flag
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __threadfence_system();
-    if (lane == 0) __hip_atomic_store(a.host_rec + 4 * pd.slot, (int)a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0)
+      __hip_atomic_store(a.host_rec + kHostRecInts * pd.slot, (int)a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -1043,9 +1063,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (from_above) g = __hip_atomic_load((gu64*)(gin + gk), BITS_RLX);
     bool ok = true;
     u64 cyc_wait = 0, cyc_wait0 = 0, n_wait = 0;  // (verbose >= 2 timeline)
+    // fill-vs-walk guard: G(m, n) = -sum of v down column n (G-space borders are
+    // 0), so each band adds minus the vertical differences of its rows < m at
+    // column n - 1 (0-based), taken by lane t at step n - 1 + t: the steps of
+    // super-blocks sbe .. nsb - 1 only
+    const int capc = pd.n - 1;
+    const bool want_end = a.endv != nullptr;
+    const int sbe = want_end ? (capc >> 6 > 1 ? capc >> 6 : 1) : nsb;
+    const int capx = want_end ? capc : -1000;
+    int cnt = 0;
+    unsigned rowm = 0;
+    {
+      const int nvr = pd.m - R0 - 32 * lane;
+      rowm = nvr >= 32 ? ~0u : (nvr <= 0 ? 0u : (1u << nvr) - 1u);
+    }
 
-    auto half = [&](int h, auto mask_t) {
+    auto half = [&](int h, auto mask_t, auto end_t) {
       constexpr bool MASK = decltype(mask_t)::value;
+      constexpr bool END = decltype(end_t)::value;
       const unsigned* wp = ywp + 64 * (h + 1);
       const unsigned nx0 = wp[0], nx1 = wp[1];  // the next half's window
       if (from_above) {
@@ -1081,7 +1116,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         // lane's words of it hold a cell within bits_w columns of the diagonal
         const bool sto = (unsigned)rel < (unsigned)nblk && (!win || bits_lane_stored(hi0 + (int64_t)s0 * pd.m, lim, hlim));
         unsigned* st = mb + (int64_t)rel * 1024;
-        col_block<NP, SR, MASK, B == 3, B>(s0, lane, x0, x1, wc0, wc1, l, c, acc, inj, pub, st, sto);
+        col_block<NP, SR, MASK, B == 3, B, END>(s0, lane, x0, x1, wc0, wc1, l, c, acc, inj, pub, st, sto, capx, rowm,
+                                                cnt);
       };
       blk(std::integral_constant<int, 0>{});
       blk(std::integral_constant<int, 1>{});
@@ -1099,15 +1135,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       wc0 = nx0;
       wc1 = nx1;
     };
-    // the first super-block (columns < 0 masked) peeled off the loop
-    half(0, std::true_type{});
-    half(1, std::true_type{});
-    for (int sb = 1; sb < nsb && ok; ++sb) {
-      half(2 * sb, std::false_type{});
-      half(2 * sb + 1, std::false_type{});
+    // the first super-block (columns < 0 masked) peeled off the loop; the last
+    // ones (column n - 1) take the guard's end value
+    // (always the END form: an if / else around the peeled halves makes the
+    // compiler treat the SGPR carries as divergent; capx = -1000 matches nothing)
+    half(0, std::true_type{}, std::true_type{});
+    half(1, std::true_type{}, std::true_type{});
+    int sb = 1;
+    for (; sb < sbe && ok; ++sb) {
+      half(2 * sb, std::false_type{}, std::false_type{});
+      half(2 * sb + 1, std::false_type{}, std::false_type{});
+    }
+    for (; sb < nsb && ok; ++sb) {
+      half(2 * sb, std::false_type{}, std::true_type{});
+      half(2 * sb + 1, std::false_type{}, std::true_type{});
     }
     BITS_PROG(0x30000000u);
     if (!ok) return;
+    if (want_end) {  // this band's part of H(m, n): - sum v (+ (m + n) pgap once, band 0)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+      if (lane == 0)
+        __hip_atomic_fetch_add((gu32*)(a.endv + pd.slot), (unsigned)(band == 0 ? (pd.m + pd.n) * a.pgap - cnt : -cnt),
+                               BITS_RLX);
+    }
     if (a.stamps && lane == 0) {  // per pair: band cycles
       atomicAdd(a.stamps + 8 * pd.slot + 6, (u64)(__builtin_amdgcn_s_memtime() - t_task));
       atomicAdd(a.stamps + 8 * pd.slot + 7, cyc_wait);

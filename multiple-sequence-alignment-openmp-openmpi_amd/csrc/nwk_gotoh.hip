@@ -238,6 +238,17 @@ __device__ __forceinline__ void trace_gotoh(const FillArgs& a, const PairDesc& p
   bool out = false;
   u64 n_sw = 0, n_dem = 0, c_wait = 0;  // (verbose >= 2 timeline: tile switches, demand loads, cycles waiting on tiles)
   const u64 c0 = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+  if (a.dbg_corrupt == pd.slot + 1) {
+    // (tests of the fill-vs-walk guard) flip the stored D bit of cell (m, n):
+    // row-lane rl / 32, bit rl % 32 of the D word at step n + rl
+    const int r = pd.m - 1, band = r >> 11, rl = r & (kBR - 1), s = pd.n + rl;
+    const int rel = (s >> 2) - gotoh_blk_lo(band, pd.m, pd.n, pd.bits_w);
+    if (lane == 0 && (unsigned)rel < (unsigned)nblk)
+      __hip_atomic_fetch_xor((gu32*)(a.mat + pd.mat_off + ((int64_t)band * nblk + rel) * 1024 + (s & 2) * 64 +
+                                     2 * (rl >> 5) + (s & 1)),
+                             1u << (rl & 31), BITS_RLX);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   while (w.i > 0 && w.j > 0 && w.k < kcap) {
     const int r = w.i - 1, band = r >> 11, rl = r & (kBR - 1), g = rl >> 6, s = w.j + rl;
     if (band != cur.band || g != cur.g || s < 64 * cur.u || s > 64 * cur.u + 127) {
@@ -376,6 +387,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
     unsigned hi0 = ywp[-64], hi1 = ywp[-63], lo0 = ywp[0], lo1 = ywp[1];
     const int nseg = kmax + 65;  // the last chunk is published after segment kmax + 64
     bool ok = true;
+    // fill-vs-walk guard: with v = G(i-1, j) - G(i, j) = VLO + (its planes set)
+    // and G(0, n) = go, H(m, n) = go + (m + n) ge - sum_i v(i, n); row
+    // 32 t + b reaches column n at step n + 32 t + b (segments kmax ..)
+    const int capn = a.endv ? pd.n : -100000;
+    int cnt = 0;  // planes set over this band's rows < m at column n
+    unsigned rowm;
+    {
+      const int nvr = pd.m - R0 - 32 * lane;
+      rowm = nvr >= 32 ? ~0u : (nvr <= 0 ? 0u : (1u << nvr) - 1u);
+    }
     for (int j = 0; j < nseg; ++j) {
       // --- the row above for lane 0's columns 32 j .. 32 j + 31 -> cons (bit 31 per column)
       {
@@ -411,8 +432,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
       }
       const unsigned* yn = ywp + 64 * (j + 1);
       const unsigned nlo0 = yn[0], nlo1 = yn[1];
-      auto seg = [&](auto mask_t) {
+      auto seg = [&](auto mask_t, auto end_t) {
         constexpr bool MASK = decltype(mask_t)::value;
+        constexpr bool END = decltype(end_t)::value;
         unsigned dq[4][2];
 #pragma unroll 4
         for (int r = 0; r < 32; ++r) {
@@ -450,6 +472,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
           step<C>(match, v, e, U, fU, vn, en, h, f, D, Fs, Ee, Fe);
 #pragma unroll
           for (int p = 0; p < NV; ++p) v[p] = vn[p];
+          if constexpr (END) {  // column n: bit s - n - 32 lane (rows < m)
+            const int bb = s - capn - 32 * lane;
+            const unsigned mk = (unsigned)bb < 32u ? (1u << bb) & rowm : 0u;
+#pragma unroll
+            for (int p = 0; p < NV; ++p) cnt += __builtin_popcount(vn[p] & mk);
+          }
 #pragma unroll
           for (int q = 0; q < NQ1; ++q) e[q] = en[q];
           if constexpr (MASK) {  // columns <= 0 keep the left border
@@ -489,8 +517,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
           }
         }
       };
-      if (j < 65) seg(std::true_type{});
-      else seg(std::false_type{});
+      if (j < 65) seg(std::true_type{}, std::true_type{});
+      else if (j >= kmax) seg(std::false_type{}, std::true_type{});
+      else seg(std::false_type{}, std::false_type{});
       hi0 = lo0;
       hi1 = lo1;
       lo0 = nlo0;
@@ -511,6 +540,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
       }
     }
     if (!ok) return;
+    if (a.endv) {  // this band's part of H(m, n) (+ the border terms once, band 0)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+      const int rows = min(kBR, pd.m - R0);
+      const int part = rows * GO - cnt + (band == 0 ? GO + (pd.m + pd.n) * GE : 0);
+      if (lane == 0) __hip_atomic_fetch_add((gu32*)(a.endv + pd.slot), (unsigned)part, BITS_RLX);
+    }
     if (a.stamps && lane == 0) {  // per pair: band cycles, of which waiting on the band above
       atomicAdd(a.stamps + 8 * pd.slot + 6, (u64)(__builtin_amdgcn_s_memtime() - t_task));
       atomicAdd(a.stamps + 8 * pd.slot + 7, cyc_wait);

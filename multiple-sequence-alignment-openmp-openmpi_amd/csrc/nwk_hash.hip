@@ -91,9 +91,14 @@ __global__ __launch_bounds__(256) void nw_rows(HashArgs h) {
   for (int o = 32; o > 0; o >>= 1) pen += __shfl_xor(pen, o);
   if (lane == 0) sp[w] = pen;
   __syncthreads();
-  if (tid == 0)
-    h.penalties[pd.slot] =
-        (int)(sp[0] + sp[1] + sp[2] + sp[3] + (pre > 0 ? h.gopen + (long long)(pre - 1) * h.gext : 0));
+  if (tid == 0) {
+    const int p = (int)(sp[0] + sp[1] + sp[2] + sp[3] + (pre > 0 ? h.gopen + (long long)(pre - 1) * h.gext : 0));
+    h.penalties[pd.slot] = p;
+    // the fill-vs-walk guard (skel:274): a walk that read a wrong code gives a
+    // path whose cost is not the fill's H(m, n) -- never published, re-run
+    // (a pair whose walk left its storage window, retry 1, has no path here)
+    if (h.endv && h.retry[pd.slot] == 0 && p != h.endv[pd.slot]) h.retry[pd.slot] = 2;
+  }
 }
 
 // SHA-512 of one materialised row per lane (lane 2q: align1 of pair q, lane

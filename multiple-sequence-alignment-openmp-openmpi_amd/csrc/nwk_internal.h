@@ -189,7 +189,18 @@ struct FillArgs {
   // (flag last, system scope), so host threads finalize pairs during the launch.
   uint8_t* ops_host;
   int* host_rec;
+  // Fill-vs-walk guard (skel:274 `ret = dp[m][n]`): per slot, the fill's own
+  // H(m, n), accumulated by the band tasks with agent-scope atomic adds onto a
+  // zeroed word before they release (bit-plane kernels: -sum of the vertical
+  // differences down column n per band, plus the border term; value kernels:
+  // the cell itself).  Every finalize compares it with the cost of the walked
+  // path and re-runs a pair that disagrees (retry[slot] = 2) instead of
+  // publishing it.  nullptr: the kernel does not provide it.
+  int* endv;
+  int dbg_corrupt;         // debug (tests): slot + 1 whose stored code of cell (m, n) is flipped before its walk
 };
+// host_rec ints per slot: {flag, length, end i, end j, fill end value H(m, n), -, -, -}
+constexpr int kHostRecInts = 8;
 constexpr int kProfSyms = 6;  // kProfileDP: symbols + gap per column profile
 
 constexpr int kMaxSegsPerPair = 16384;  // segment ids are 14 bits in the traceback records
@@ -208,6 +219,8 @@ struct HashArgs {
   int pxy, gopen, gext;    // move costs (linear: gopen = gext = pgap)
   int* penalties;          // per slot
   uint8_t* hashes;         // per slot, 64 raw bytes
+  const int* endv;         // per slot: the fill's H(m, n) (FillArgs::endv), nullptr = unchecked
+  int* retry;              // per slot: set to 2 when the walked path's cost differs from endv
 };
 hipError_t launch_hash(const HashArgs& h, hipStream_t s);
 

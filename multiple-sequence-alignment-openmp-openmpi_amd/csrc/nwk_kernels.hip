@@ -44,11 +44,30 @@ __device__ __forceinline__ void st_granule(u64* p, unsigned epoch, int v) {
   __hip_atomic_store((gu64*)p, ((u64)epoch << 32) | (unsigned)v, RLX_AGENT);
 }
 
-// Loads the compiler does not track.  The block loop issues its prefetch
-// loads here and waits for them itself with a COUNTED s_waitcnt right after
-// the block's stores (vmcnt counts loads and stores together, in order): the
-// compiler's own loop-header vmcnt(0) would otherwise make every block wait
-// for the previous block's HBM stores to complete.
+// The block loops' prefetch loads (next super-block's E / SEL words and
+// band-above granules, issued one super-block ahead) and their waits.
+//
+// Until round 6 these were inline-asm loads the compiler did not track, waited
+// for by a COUNTED s_waitcnt after the block's stores (the compiler's own
+// loop-header vmcnt(0) would make every block wait for the previous block's
+// stores).  That form is unsound: the compiler believes an asm output is ready
+// when the asm statement ends, and where it needs the "+v" operands of the
+// wait in other registers (a join of the block variants) it copies the
+// in-flight destinations BEFORE the wait -- v_mov of a register the load has
+// not written yet.  A late load then leaves the previous super-block's value
+// in the copy; for a granule that is the previous chunk's (same epoch: it
+// passes the tag check), so a band pair computes from a wrong upper row.  This
+// was nw_align_pka's intermittent wrong penalty (round 5: 2-6% of runs of its
+// windowed job, found in round 6 by the fill-vs-walk guard, which saw the
+// FILL's H(m, n) below the true minimum, and then in the ISA: nw_align_pka
+// .LBB7_113 copies v85/v131/v[16:17]/v[18:19] before the s_waitcnt; the same
+// shape in nw_align, nw_align_pk, nw_align_pk2 and nw_align_affine).  The
+// loads are now ordinary (compiler-tracked) loads, which the compiler waits
+// for before any use or copy; NWK_ASM_PREFETCH=1 builds the old form (A/B).
+#ifndef NWK_ASM_PREFETCH
+#define NWK_ASM_PREFETCH 0
+#endif
+#if NWK_ASM_PREFETCH
 __device__ __forceinline__ void asm_load_E(const unsigned* p, unsigned& e0, unsigned& e1) {
   asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %2, off offset:16"
                : "=&v"(e0), "=&v"(e1)
@@ -71,10 +90,25 @@ __device__ __forceinline__ void wait_vm_keep(unsigned& a, unsigned& b, u64& c) {
   static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
   asm volatile("s_waitcnt vmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "n"(N) : "memory");
 }
+#else
+__device__ __forceinline__ void asm_load_E(const unsigned* p, unsigned& e0, unsigned& e1) {
+  e0 = p[0];
+  e1 = p[4];
+}
+__device__ __forceinline__ void asm_load_E2(const unsigned* p, unsigned& e0, unsigned& e1) {
+  e0 = p[0];
+  e1 = p[64];
+}
+// (an 8-byte sc1 load: a granule is read untorn)
+__device__ __forceinline__ void asm_load_granule(const u64* p, u64& v) { v = __hip_atomic_load((gu64*)p, RLX_AGENT); }
+template <int N>
+__device__ __forceinline__ void wait_vm_keep(unsigned&, unsigned&, u64&) {}
+#endif
 
 // The same, but waits for every outstanding op when `all` (wave-uniform) is
 // set -- one asm block, so the compiler never copies a register between two
 // differently counted waits (a copy made before the wait reads the old value).
+#if NWK_ASM_PREFETCH
 template <int N>
 __device__ __forceinline__ void wait_vm_keep_or_all(bool all, unsigned& a, unsigned& b, u64& c) {
   static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
@@ -88,6 +122,10 @@ __device__ __forceinline__ void wait_vm_keep_or_all(bool all, unsigned& a, unsig
       : [all] "s"(__builtin_amdgcn_readfirstlane(all ? 1 : 0)), [n] "n"(N)
       : "memory", "scc");
 }
+#else
+template <int N>
+__device__ __forceinline__ void wait_vm_keep_or_all(bool, unsigned&, unsigned&, u64&) {}
+#endif
 
 // A zero the optimiser cannot see: LLVM rewrites an idempotent atomic RMW
 // (add 0) into a plain atomic load, which can be served by a stale copy in
@@ -175,11 +213,13 @@ __device__ __forceinline__ int cell(int dg, int up, int left, unsigned ysh, unsi
 // Eight wavefront steps s0..s0+7 (s0 % 8 == 0).
 //   bslot: LDS ring holding B[s0+1 .. s0+8] (the band-above row, G-space)
 //   mptr:  this lane's store pointer for the block's first dword row
-template <int MODE, int W, bool MASK>
+// CAPT: the block of cell (m, n): hs := every row's G after step s0 + kcap
+// (the fill-vs-walk guard's end value, FillArgs::endv)
+template <int MODE, int W, bool MASK, bool CAPT = false>
 __device__ __forceinline__ void step_block(int s0, int lane, int (&h)[kRows], int& Up, int& stage,
                                            unsigned (&acc)[kRows], const unsigned (&xq)[kRows],
                                            unsigned e0, unsigned e1, const int* bslot,
-                                           unsigned* mptr, int K0, int K1, bool store = true) {
+                                           unsigned* mptr, int K0, int K1, bool store, int kcap, int (&hs)[kRows]) {
   constexpr int SPD = 32 / W;
   const int4 bA = *reinterpret_cast<const int4*>(bslot);
   const int4 bB = *reinterpret_cast<const int4*>(bslot + 4);
@@ -207,6 +247,12 @@ __device__ __forceinline__ void step_block(int s0, int lane, int (&h)[kRows], in
     }
 #pragma unroll
     for (int r = 0; r < kRows; ++r) h[r] = hn[r];
+    if constexpr (CAPT) {
+      if (k == kcap) {
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) hs[r] = hn[r];
+      }
+    }
     if constexpr (W < 32) {
 #pragma unroll
       for (int r = 0; r < kRows; ++r) acc[r] = __builtin_amdgcn_alignbit((unsigned)h[r], acc[r], W);
@@ -728,6 +774,19 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
     const u64 t_task = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
     // stores one block issues after its prefetch loads (<= 63: vmcnt field)
     constexpr int kBlockStores = (8 / SPD) * kRows > 63 ? 63 : (8 / SPD) * kRows;
+    // fill-vs-walk guard: cell (m, n) is lane t's row r of band (m - 1) / 512
+    // at step n - 1 + t (the plain fill and the linear-space fill pass)
+    int cap_s0 = -1, cap_s = 0, cap_t = 0, cap_r = 0;
+    int hs[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) hs[r] = 0;
+    if (a.endv && a.lin_mode != 2 && band == (pd.m - 1) / kBandRows) {
+      const int wr = (pd.m - 1) % kBandRows;
+      cap_t = wr / kRows;
+      cap_r = wr % kRows;
+      cap_s = pd.n - 1 + cap_t;
+      cap_s0 = cap_s & ~7;
+    }
 
     for (int sb = 0; sb < pd.sblocks; ++sb) {
       // --- band-above row for this super-block: B[64sb+1 .. 64sb+64] = chunk sb+1
@@ -763,10 +822,15 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
         const int s0 = sb * 64 + blk * 8;
         // this lane's columns for steps s0..s0+7: E[s0 - lane], E[s0 - lane + 4]
         const unsigned e0 = ewin[blk * 8 + 64 - lane], e1 = ewin[blk * 8 + 68 - lane];
-        if (sb == 0)
-          step_block<MODE, W, true>(s0, lane, h, Up, stage, acc, xq, e0, e1, slot + blk * 8, mptr, a.K0, a.K1, store);
+        if (s0 == cap_s0)  // the block of cell (m, n)
+          step_block<MODE, W, true, true>(s0, lane, h, Up, stage, acc, xq, e0, e1, slot + blk * 8, mptr, a.K0, a.K1,
+                                          store, cap_s & 7, hs);
+        else if (sb == 0)
+          step_block<MODE, W, true>(s0, lane, h, Up, stage, acc, xq, e0, e1, slot + blk * 8, mptr, a.K0, a.K1, store,
+                                    0, hs);
         else
-          step_block<MODE, W, false>(s0, lane, h, Up, stage, acc, xq, e0, e1, slot + blk * 8, mptr, a.K0, a.K1, store);
+          step_block<MODE, W, false>(s0, lane, h, Up, stage, acc, xq, e0, e1, slot + blk * 8, mptr, a.K0, a.K1, store,
+                                     0, hs);
         mptr += (8 / SPD) * kRows * kWave;
         // the window / granule prefetches are older than this block's
         // kBlockStores stores: waiting for the rest leaves those in flight
@@ -779,6 +843,13 @@ __global__ __launch_bounds__(256) void nw_align(FillArgs a) {
       __builtin_amdgcn_wave_barrier();
     }
     if (!ok) return;
+    if (cap_s0 >= 0) {  // H(m, n) = G(m, n) + (m + n) pgap
+      int v = hs[0];
+#pragma unroll
+      for (int r = 1; r < kRows; ++r) v = cap_r == r ? hs[r] : v;
+      if (lane == cap_t)
+        __hip_atomic_fetch_add((gu32*)(a.endv + pd.slot), (unsigned)(v + (pd.m + pd.n) * a.pgap), RLX_AGENT);
+    }
     // --- band finished: make its stores visible at agent scope, then count
     // it (MI355X_MICROARCH.md R1: drain -> release fence -> drain -> counter).
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -978,6 +1049,7 @@ __device__ __forceinline__ unsigned pk_add(unsigned a, unsigned b) {
 __device__ __forceinline__ unsigned pk_sub(unsigned a, unsigned b) {
   return __builtin_bit_cast(unsigned, __builtin_bit_cast(s16x2, a) - __builtin_bit_cast(s16x2, b));
 }
+#if NWK_ASM_PREFETCH
 __device__ __forceinline__ void asm_load_S3(const unsigned* p, unsigned& a, unsigned& b, unsigned& c) {
   asm volatile(
       "global_load_dword %0, %3, off\n\tglobal_load_dword %1, %3, off offset:256\n\t"
@@ -986,21 +1058,34 @@ __device__ __forceinline__ void asm_load_S3(const unsigned* p, unsigned& a, unsi
       : "v"(p)
       : "memory");
 }
+#else
+__device__ __forceinline__ void asm_load_S3(const unsigned* p, unsigned& a, unsigned& b, unsigned& c) {
+  a = p[0];
+  b = p[64];
+  c = p[128];
+}
+#endif
+#if NWK_ASM_PREFETCH
 template <int N>
 __device__ __forceinline__ void wait_vm_keep3(unsigned& a, unsigned& b, unsigned& c, u64& d) {
   static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
   asm volatile("s_waitcnt vmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N) : "memory");
 }
+#else
+template <int N>
+__device__ __forceinline__ void wait_vm_keep3(unsigned&, unsigned&, unsigned&, u64&) {}
+#endif
 
 // Eight wavefront steps s0..s0+7 (s0 % 8 == 0).
 //   bslot: LDS ring of (B[s0+1 .. s0+8] - base) << 16 (band-above row)
 //   srow:  LDS SEL window at this lane's column for step s0 (8 words)
 //   pub:   publish the stage window after the stage shift of step 7
-template <bool MASK>
+// CAPT: the block of cell (m, n): Ps := every row pair after step s0 + kcap (FillArgs::endv)
+template <bool MASK, bool CAPT = false>
 __device__ __forceinline__ void step_block_pk(int s0, int lane, unsigned (&P)[4], unsigned& U, unsigned& stage,
                                               const unsigned (&pl)[4], const unsigned (&ph)[4], const unsigned* srow,
                                               const int* bslot, unsigned* mptr, bool pub, u64* gpub, unsigned epoch,
-                                              int base) {
+                                              int base, int kcap, unsigned (&Ps)[4]) {
   const int4 bA = *reinterpret_cast<const int4*>(bslot);
   const int4 bB = *reinterpret_cast<const int4*>(bslot + 4);
   const int bv[8] = {bA.x, bA.y, bA.z, bA.w, bB.x, bB.y, bB.z, bB.w};
@@ -1033,6 +1118,12 @@ __device__ __forceinline__ void step_block_pk(int s0, int lane, unsigned (&P)[4]
       const unsigned M = s > 2 * lane ? 0xffffffffu : (s == 2 * lane ? 0x0000ffffu : 0u);
 #pragma unroll
       for (int q = 0; q < 4; ++q) Pn[q] &= M;
+    }
+    if constexpr (CAPT) {
+      if (k == kcap) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Ps[q] = Pn[q];
+      }
     }
     if (k & 1) {
 #pragma unroll
@@ -1113,6 +1204,17 @@ __global__ __launch_bounds__(256) void nw_align_pk(FillArgs a) {
     constexpr int kBlockStores = 8;
     u64 cyc_wait = 0, cyc_wait0 = 0, n_wait = 0;
     const u64 t_task = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+    // fill-vs-walk guard: cell (m, n) is lane t's row r of the last band, held
+    // in P[r & 3] (low half r < 4, high half r >= 4) at step n - 1 + 2t + (r >> 2)
+    int cap_s0 = -1, cap_s = 0, cap_t = 0, cap_r = 0, cap_base = 0;
+    unsigned Ps[4] = {0u, 0u, 0u, 0u};
+    if (a.endv && band == pd.nbands - 1) {
+      const int wr = (pd.m - 1) - band * kBandRows;
+      cap_t = wr / kRows;
+      cap_r = wr % kRows;
+      cap_s = pd.n - 1 + 2 * cap_t + (cap_r >> 2);
+      cap_s0 = cap_s & ~7;
+    }
 
     for (int sb = 0; sb < pd.sblocks; ++sb) {
       // --- band-above row for this super-block: B[64sb+1 .. 64sb+64] = chunk sb
@@ -1159,16 +1261,31 @@ __global__ __launch_bounds__(256) void nw_align_pk(FillArgs a) {
         const int s0 = sb * 64 + blk * 8;
         const unsigned* srow = w + blk * 8 + 128 - 2 * lane;
         const bool pub = pub_sb && blk == 7;
-        if (sb < 2)
-          step_block_pk<true>(s0, lane, P, U, stage, pl, ph, srow, slot + blk * 8, mptr, pub, gpub, a.epoch, base);
+        if (s0 == cap_s0) {  // the block of cell (m, n)
+          step_block_pk<true, true>(s0, lane, P, U, stage, pl, ph, srow, slot + blk * 8, mptr, pub, gpub, a.epoch,
+                                    base, cap_s & 7, Ps);
+          cap_base = base;
+        } else if (sb < 2)
+          step_block_pk<true>(s0, lane, P, U, stage, pl, ph, srow, slot + blk * 8, mptr, pub, gpub, a.epoch, base, 0,
+                              Ps);
         else
-          step_block_pk<false>(s0, lane, P, U, stage, pl, ph, srow, slot + blk * 8, mptr, pub, gpub, a.epoch, base);
+          step_block_pk<false>(s0, lane, P, U, stage, pl, ph, srow, slot + blk * 8, mptr, pub, gpub, a.epoch, base, 0,
+                               Ps);
         mptr += 2 * 4 * kWave;
         wait_vm_keep3<kBlockStores>(sw0, sw1, sw2, pend);
       }
       __builtin_amdgcn_wave_barrier();
     }
     if (!ok) return;
+    if (cap_s0 >= 0) {  // H(m, n) = G + (m + n) pgap, G = the half (int16) + base
+      const int q = cap_r & 3;
+      unsigned v = Ps[0];
+#pragma unroll
+      for (int r = 1; r < 4; ++r) v = q == r ? Ps[r] : v;
+      const int g = (int)(short)(cap_r >= 4 ? v >> 16 : v & 0xffffu) + cap_base;
+      if (lane == cap_t)
+        __hip_atomic_fetch_add((gu32*)(a.endv + pd.slot), (unsigned)(g + (pd.m + pd.n) * a.pgap), RLX_AGENT);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1199,11 +1316,13 @@ __global__ __launch_bounds__(256) void nw_align_pk(FillArgs a) {
 //   bslot: LDS ring of B[s0+1 .. s0+8] - base (band-above row, low 16 bits)
 //   srow:  LDS SEL64 window at this lane's column for step s0 (8 words)
 //   upsel: v_perm selector of up0: lane 0 {B, lane 63's band-2p row}, others identity
-template <bool MASK>
+// CAPT: the block of cell (m, n): Ps := every row pair after step s0 + kcap (FillArgs::endv)
+template <bool MASK, bool CAPT = false>
 __device__ __forceinline__ void step_block_pk2(int s0, int lane, unsigned (&P)[kRows], unsigned& U, unsigned& stage,
                                                const unsigned (&pl)[kRows], const unsigned (&ph)[kRows],
                                                const unsigned* srow, const int* bslot, unsigned upsel, unsigned* mptr,
-                                               bool pub, u64* gpub, unsigned epoch, int base) {
+                                               bool pub, u64* gpub, unsigned epoch, int base, int kcap,
+                                               unsigned (&Ps)[kRows]) {
   const int4 bA = *reinterpret_cast<const int4*>(bslot);
   const int4 bB = *reinterpret_cast<const int4*>(bslot + 4);
   const int bv[8] = {bA.x, bA.y, bA.z, bA.w, bB.x, bB.y, bB.z, bB.w};
@@ -1237,6 +1356,12 @@ __device__ __forceinline__ void step_block_pk2(int s0, int lane, unsigned (&P)[k
 #pragma unroll
       for (int r = 0; r < kRows; ++r) Pn[r] &= M;
     }
+    if constexpr (CAPT) {
+      if (k == kcap) {
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) Ps[r] = Pn[r];
+      }
+    }
     if (k & 1) {
 #pragma unroll
       for (int r = 0; r < kRows; ++r) {
@@ -1255,12 +1380,19 @@ __device__ __forceinline__ void step_block_pk2(int s0, int lane, unsigned (&P)[k
   }
 }
 
+#if NWK_ASM_PREFETCH
 __device__ __forceinline__ void asm_load_S2(const unsigned* p, unsigned& a, unsigned& b) {
   asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %2, off offset:256"
                : "=&v"(a), "=&v"(b)
                : "v"(p)
                : "memory");
 }
+#else
+__device__ __forceinline__ void asm_load_S2(const unsigned* p, unsigned& a, unsigned& b) {
+  a = p[0];
+  b = p[64];
+}
+#endif
 
 __global__ __launch_bounds__(256) void nw_align_pk2(FillArgs a) {
   constexpr int W = 4;
@@ -1328,6 +1460,20 @@ __global__ __launch_bounds__(256) void nw_align_pk2(FillArgs a) {
     constexpr int kBlockStores = 2 * kRows;
     u64 cyc_wait = 0, cyc_wait0 = 0, n_wait = 0;
     const u64 t_task = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+    // fill-vs-walk guard: cell (m, n) is row (m - 1) % 1024 of the last band
+    // pair -- half h, lane t, row r -- at step n - 1 + t + 64 h (Lay<4, 2>)
+    int cap_s0 = -1, cap_s = 0, cap_t = 0, cap_r = 0, cap_h = 0, cap_base = 0;
+    unsigned Ps[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) Ps[r] = 0;
+    if (a.endv && bp == ntp - 1) {
+      const int wr = (pd.m - 1) - 2 * bp * kBandRows;
+      cap_h = wr >= kBandRows ? 1 : 0;
+      cap_t = (wr - cap_h * kBandRows) / kRows;
+      cap_r = (wr - cap_h * kBandRows) % kRows;
+      cap_s = pd.n - 1 + cap_t + 64 * cap_h;
+      cap_s0 = cap_s & ~7;
+    }
 
     for (int sb = 0; sb < pd.sblocks; ++sb) {
       // --- band-above row for this super-block: B[64sb+1 .. 64sb+64] = chunk sb
@@ -1373,18 +1519,30 @@ __global__ __launch_bounds__(256) void nw_align_pk2(FillArgs a) {
         const int s0 = sb * 64 + blk * 8;
         const unsigned* srow = w + blk * 8 + 64 - lane;
         const bool pub = pub_sb && blk == 7;
-        if (sb < 2)
+        if (s0 == cap_s0) {  // the block of cell (m, n)
+          step_block_pk2<true, true>(s0, lane, P, U, stage, pl, ph, srow, slot + blk * 8, upsel, mptr, pub, gpub,
+                                     a.epoch, base, cap_s & 7, Ps);
+          cap_base = base;
+        } else if (sb < 2)
           step_block_pk2<true>(s0, lane, P, U, stage, pl, ph, srow, slot + blk * 8, upsel, mptr, pub, gpub, a.epoch,
-                               base);
+                               base, 0, Ps);
         else
           step_block_pk2<false>(s0, lane, P, U, stage, pl, ph, srow, slot + blk * 8, upsel, mptr, pub, gpub, a.epoch,
-                                base);
+                                base, 0, Ps);
         mptr += 2 * kRows * kWave;
         wait_vm_keep<kBlockStores>(sw0, sw1, pend);
       }
       __builtin_amdgcn_wave_barrier();
     }
     if (!ok) return;
+    if (cap_s0 >= 0) {  // H(m, n) = G + (m + n) pgap, G = the half (int16) + base
+      unsigned v = Ps[0];
+#pragma unroll
+      for (int r = 1; r < kRows; ++r) v = cap_r == r ? Ps[r] : v;
+      const int g = (int)(short)(cap_h ? v >> 16 : v & 0xffffu) + cap_base;
+      if (lane == cap_t)
+        __hip_atomic_fetch_add((gu32*)(a.endv + pd.slot), (unsigned)(g + (pd.m + pd.n) * a.pgap), RLX_AGENT);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1468,12 +1626,13 @@ hipError_t launch_gather(const FillArgs& a, int npairs, int task_shift, hipStrea
 // ===========================================================================
 constexpr int kAffInf = 0x3fffffff;
 
-template <bool MASK>
+// CAPT: the block of cell (m, n): hs := every row's H after step s0 + kcap (FillArgs::endv)
+template <bool MASK, bool CAPT = false>
 __device__ __forceinline__ void step_block_affine(int s0, int lane, int (&h)[kRows], int (&e)[kRows], int& Up,
                                                   int& f7, int& stH, int& stF, unsigned (&acc)[kRows],
                                                   const unsigned (&xq)[kRows], unsigned e0, unsigned e1,
                                                   const int* bH, const int* bF, unsigned* mptr, int pxy, int goe,
-                                                  int ge) {
+                                                  int ge, int kcap, int (&hs)[kRows]) {
   const int4 hA = *reinterpret_cast<const int4*>(bH), hB = *reinterpret_cast<const int4*>(bH + 4);
   const int4 fA = *reinterpret_cast<const int4*>(bF), fB = *reinterpret_cast<const int4*>(bF + 4);
   const int bh[8] = {hA.x, hA.y, hA.z, hA.w, hB.x, hB.y, hB.z, hB.w};
@@ -1518,6 +1677,12 @@ __device__ __forceinline__ void step_block_affine(int s0, int lane, int (&h)[kRo
     }
 #pragma unroll
     for (int r = 0; r < kRows; ++r) { h[r] = hn[r]; e[r] = en[r]; }
+    if constexpr (CAPT) {
+      if (k == kcap) {
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) hs[r] = hn[r];
+      }
+    }
     f7 = fprev;
     if (k == 7) {
 #pragma unroll
@@ -1527,10 +1692,15 @@ __device__ __forceinline__ void step_block_affine(int s0, int lane, int (&h)[kRo
   }
 }
 
+#if NWK_ASM_PREFETCH
 template <int N>
 __device__ __forceinline__ void wait_vm_keep4(unsigned& a, unsigned& b, u64& c, u64& d) {
   asm volatile("s_waitcnt vmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N) : "memory");
 }
+#else
+template <int N>
+__device__ __forceinline__ void wait_vm_keep4(unsigned&, unsigned&, u64&, u64&) {}
+#endif
 
 // Traceback of one affine pair on its 4-bit codes (same LDS tile staging as
 // trace_pair).  Per 8x8 block every lane loads its cell's code; the walk is
@@ -1757,6 +1927,18 @@ __global__ __launch_bounds__(256) void nw_align_affine(FillArgs a) {
     wait_vm_keep4<0>(ew0, ew1, pH, pF);
     bool ok = true;
     constexpr int kBlockStores = kRows;
+    // fill-vs-walk guard: cell (m, n) is lane t's row r of the last band at step n - 1 + t
+    int cap_s0 = -1, cap_s = 0, cap_t = 0, cap_r = 0;
+    int hs[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) hs[r] = 0;
+    if (a.endv && band == pd.nbands - 1) {
+      const int wr = (pd.m - 1) - band * kBandRows;
+      cap_t = wr / kRows;
+      cap_r = wr % kRows;
+      cap_s = pd.n - 1 + cap_t;
+      cap_s0 = cap_s & ~7;
+    }
 
     for (int sb = 0; sb < pd.sblocks; ++sb) {
       PROG(0x20000000u | sb);
@@ -1787,12 +1969,15 @@ __global__ __launch_bounds__(256) void nw_align_affine(FillArgs a) {
       for (int blk = 0; blk < 8; ++blk) {
         const int s0 = sb * 64 + blk * 8;
         const unsigned e0 = ewin[blk * 8 + 64 - lane], e1 = ewin[blk * 8 + 68 - lane];
-        if (sb == 0)
+        if (s0 == cap_s0)  // the block of cell (m, n)
+          step_block_affine<true, true>(s0, lane, h, e, Up, f7, stH, stF, acc, xq, e0, e1, slH + blk * 8,
+                                        slF + blk * 8, mptr, pxy, goe, ge, cap_s & 7, hs);
+        else if (sb == 0)
           step_block_affine<true>(s0, lane, h, e, Up, f7, stH, stF, acc, xq, e0, e1, slH + blk * 8, slF + blk * 8, mptr,
-                                  pxy, goe, ge);
+                                  pxy, goe, ge, 0, hs);
         else
           step_block_affine<false>(s0, lane, h, e, Up, f7, stH, stF, acc, xq, e0, e1, slH + blk * 8, slF + blk * 8,
-                                   mptr, pxy, goe, ge);
+                                   mptr, pxy, goe, ge, 0, hs);
         mptr += (8 / SPD) * kRows * kWave;
         wait_vm_keep4<kBlockStores>(ew0, ew1, pH, pF);
       }
@@ -1804,6 +1989,12 @@ __global__ __launch_bounds__(256) void nw_align_affine(FillArgs a) {
     }
     PROG(0x30000000u);
     if (!ok) return;
+    if (cap_s0 >= 0) {  // H(m, n) (absolute)
+      int v = hs[0];
+#pragma unroll
+      for (int r = 1; r < kRows; ++r) v = cap_r == r ? hs[r] : v;
+      if (lane == cap_t) __hip_atomic_fetch_add((gu32*)(a.endv + pd.slot), (unsigned)v, RLX_AGENT);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1862,13 +2053,16 @@ __device__ __forceinline__ unsigned pk_or(unsigned a, unsigned m) { return a | m
 //   hb0:    packed border H of row 0 (masked steps), + r * ge4 for row r
 //   STO:    code stores: 1 always, 0 never (outside the stored window,
 //           PairDesc::bits_w), 2 when `sto` (the masked super-blocks)
-template <bool MASK, int STO>
+//   CAPT:   (the block of cell (m, n)) Hs := every row's H after step s0 + kcap
+//           (the fill-vs-walk guard's end value, FillArgs::endv)
+template <bool MASK, int STO, bool CAPT = false>
 __device__ __forceinline__ void step_block_pka(int s0, int lane, bool sto, unsigned (&Hc)[kRows], unsigned (&Ec)[kRows],
                                                unsigned (&Nb)[kRows], unsigned& F7, unsigned& U, unsigned& stH,
                                                unsigned& stF, const unsigned (&pl)[kRows], const unsigned (&ph)[kRows],
                                                const unsigned* srow, const int* bH, const int* bF, unsigned upsel,
                                                unsigned* mptr, bool pub, u64* gpH, u64* gpF, unsigned epoch,
-                                               int base_hi, unsigned goe4, unsigned ge4, unsigned hb0, unsigned xfer) {
+                                               int base_hi, unsigned goe4, unsigned ge4, unsigned hb0, unsigned xfer,
+                                               int kcap, unsigned (&Hs)[kRows]) {
   const int4 hA = *reinterpret_cast<const int4*>(bH), hB = *reinterpret_cast<const int4*>(bH + 4);
   const int4 fA = *reinterpret_cast<const int4*>(bF), fB = *reinterpret_cast<const int4*>(bF + 4);
   const int bh[8] = {hA.x, hA.y, hA.z, hA.w, hB.x, hB.y, hB.z, hB.w};
@@ -1927,6 +2121,12 @@ __device__ __forceinline__ void step_block_pka(int s0, int lane, bool sto, unsig
       }
     }
     F7 = fup;
+    if constexpr (CAPT) {
+      if (k == kcap) {
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) Hs[r] = Hn[r];
+      }
+    }
     if (STO == 1 || (STO == 2 && sto)) {
       if (k & 1) {
 #pragma unroll
@@ -1981,6 +2181,17 @@ __device__ __forceinline__ void trace_pair_pka(const FillArgs& a, const PairDesc
   };
   auto drain = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
   uint8_t* ops = a.ops + pd.ops_off;
+  if (a.dbg_corrupt == pd.slot + 1) {
+    // (tests of the fill-vs-walk guard) cell (m, n)'s source tag: D becomes F, F or E becomes D
+    const int w1 = pd.m - 1, b1 = w1 / kBandRows, wr = w1 - b1 * kBandRows, t1 = wr / kRows, r1 = wr - t1 * kRows;
+    const int h1 = Y::hb(b1), s1 = Y::step(t1, r1, pd.n, h1), sl = sblo_of(b1);
+    if (lane == 0 && (unsigned)((s1 >> 6) - sl) < (unsigned)nsb) {
+      unsigned* p = const_cast<unsigned*>(mb) + Y::base(b1, bdw) + ((int64_t)(s1 / SPC - 16 * sl) * RPC + r1) * kWave + t1;
+      const unsigned sh = Y::shift(s1, r1, h1), d = *p, tag = (d >> sh) & 3u;
+      *p = (d & ~(3u << sh)) | ((tag == 0u ? 1u : 0u) << sh);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   int i = pd.m, j = pd.n, Lc = 0, flushed = 0, tb = -1, tq = 0, tt0 = 0, tsb = 0;
   unsigned st = 0;  // 0 = H, 1 = F, 2 = E
   bool bad = false, out = false;
@@ -2195,6 +2406,20 @@ __global__ __launch_bounds__(256) NWK_PKA_OCC void nw_align_pka(FillArgs a) {
     wait_vm_keep4<0>(sw0, sw1, pH, pF);
     bool ok = true;
     constexpr int kBlockStores = 2 * kRows;
+    // fill-vs-walk guard: cell (m, n) is row (m - 1) % 1024 of this band pair
+    // when it is the last one -- half h, lane t, row r -- at step n - 1 + t + 64 h
+    int cap_s0 = -1, cap_s = 0, cap_t = 0, cap_r = 0, cap_h = 0, cap_base = 0;
+    unsigned Hs[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) Hs[r] = 0;
+    if (a.endv && bp == ntp - 1) {
+      const int wr = (pd.m - 1) - R;  // 0 .. 2 kBandRows - 1
+      cap_h = wr >= kBandRows ? 1 : 0;
+      cap_t = (wr - cap_h * kBandRows) / kRows;
+      cap_r = (wr - cap_h * kBandRows) % kRows;
+      cap_s = pd.n - 1 + cap_t + 64 * cap_h;
+      cap_s0 = cap_s & ~7;
+    }
 
     for (int sb = 0; sb < pd.sblocks; ++sb) {
       PROG(0x20000000u | (unsigned)sb);
@@ -2255,15 +2480,23 @@ __global__ __launch_bounds__(256) NWK_PKA_OCC void nw_align_pka(FillArgs a) {
         const int s0 = sb * 64 + blk * 8;
         const unsigned* srow = w + blk * 8 + 64 - lane;
         const bool pub = pub_sb && blk == 7;
-        if (sb < 2)
+        if (s0 == cap_s0) {  // the block of cell (m, n): its H (and the base it is relative to)
+          step_block_pka<true, 2, true>(s0, lane, sto, Hc, Ec, Nb, F7, U, stH, stF, pl, ph, srow, slH + blk * 8,
+                                        slF + blk * 8, upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0,
+                                        xfer, cap_s & 7, Hs);
+          cap_base = cap_h ? base_hi : base_lo;
+        } else if (sb < 2)
           step_block_pka<true, 2>(s0, lane, sto, Hc, Ec, Nb, F7, U, stH, stF, pl, ph, srow, slH + blk * 8,
-                                  slF + blk * 8, upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0, xfer);
+                                  slF + blk * 8, upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0, xfer,
+                                  0, Hs);
         else if (sto)
           step_block_pka<false, 1>(s0, lane, sto, Hc, Ec, Nb, F7, U, stH, stF, pl, ph, srow, slH + blk * 8,
-                                   slF + blk * 8, upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0, xfer);
+                                   slF + blk * 8, upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0, xfer,
+                                   0, Hs);
         else
           step_block_pka<false, 0>(s0, lane, sto, Hc, Ec, Nb, F7, U, stH, stF, pl, ph, srow, slH + blk * 8,
-                                   slF + blk * 8, upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0, xfer);
+                                   slF + blk * 8, upsel, mptr, pub, gpH, gpF, a.epoch, base_hi, goe4, ge4, hb0, xfer,
+                                   0, Hs);
         // the counted wait keeps this block's stores in flight; a block that
         // stored nothing waits for the prefetches themselves
         if (sto) {
@@ -2277,6 +2510,13 @@ __global__ __launch_bounds__(256) NWK_PKA_OCC void nw_align_pka(FillArgs a) {
     }
     PROG(0x30000000u);
     if (!ok) return;
+    if (cap_s0 >= 0) {  // H(m, n): lane cap_t's row cap_r, half cap_h (scaled, biased, relative to cap_base)
+      unsigned v = Hs[0];
+#pragma unroll
+      for (int r = 1; r < kRows; ++r) v = cap_r == r ? Hs[r] : v;
+      const int hv = (int)((cap_h ? v >> 16 : v & 0xffffu) >> 2) - kPkaBias / 4 + cap_base;
+      if (lane == cap_t) __hip_atomic_fetch_add((gu32*)(a.endv + pd.slot), (unsigned)hv, RLX_AGENT);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2389,10 +2629,22 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
     // s_waitcnt would read the register before the data landed.
     u64 pend = from_above ? ld_granule(gin) : 0;
     bool ok = true;
+    // fill-vs-walk guard: cell (m, n) is lane t's row r of the last band at
+    // step n - 1 + t; H = key / 4
+    int cap_s = -1, cap_t = 0, cap_r = 0;
+    unsigned hs[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) hs[r] = 0;
+    if (a.endv && band == pd.nbands - 1) {
+      const int wr = (pd.m - 1) - band * kBandRows;
+      cap_t = wr / kRows;
+      cap_r = wr % kRows;
+      cap_s = pd.n - 1 + cap_t;
+    }
 
     // one super-block of 64 steps; MASK: super-block 0, whose first 63 steps
     // reach lanes before their column 1 (the border H[i][0] stays)
-    auto run_sb = [&](int sb, auto maskc) {
+    auto run_sb = [&](int sb, auto maskc, int capk) {
       constexpr bool MASK = decltype(maskc)::value;
       const unsigned* slot = ring + (sb & 1) * 64;
       const int4* cw = cwin_all[wid][sb & 1];
@@ -2443,6 +2695,10 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
           }
 #pragma unroll
           for (int r = 0; r < kRows; ++r) h[r] = nh[r];  // (d above read the previous step's h[r - 1])
+          if (blk * 8 + k == capk) {  // (uniform) the step of cell (m, n): the fill-vs-walk guard's end value
+#pragma unroll
+            for (int r = 0; r < kRows; ++r) hs[r] = nh[r];
+          }
           if (k == 7) {
 #pragma unroll
             for (int r = 0; r < kRows; ++r) __builtin_nontemporal_store(acc[r], mptr + r * kWave);
@@ -2473,15 +2729,22 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
       for (int k = 0; k < 4; ++k) cw[lane + 64 * k] = colg[128 * sb + lane + 64 * k];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
+      const int capk = cap_s >= 0 && cap_s >> 6 == sb ? cap_s & 63 : -1;
       if (sb == 0)
-        run_sb(sb, std::true_type{});
+        run_sb(sb, std::true_type{}, capk);
       else
-        run_sb(sb, std::false_type{});
+        run_sb(sb, std::false_type{}, capk);
       if (to_below && sb >= 1 && sb <= pd.nchunks) st_granule(gout + 64 * (sb - 1), a.epoch, (int)stH);
       __builtin_amdgcn_wave_barrier();
       PROG(0x20000000u | ((unsigned)band << 12) | (unsigned)(sb & 0xfff));
     }
     if (!ok) return;
+    if (cap_s >= 0) {
+      unsigned v = hs[0];
+#pragma unroll
+      for (int r = 1; r < kRows; ++r) v = cap_r == r ? hs[r] : v;
+      if (lane == cap_t) __hip_atomic_fetch_add((gu32*)(a.endv + pd.slot), v >> 2, RLX_AGENT);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -136,6 +136,7 @@ struct PairWork {
   int64_t njobs;                  // queued extra guesses (spec boundaries x (nguess - 1))
   int bits_w = 0;                 // kBits windowed storage: half-width in columns (0 = full), see PairDesc
   int bits_nblk = 0;              // kBits: stored 8-step blocks per band
+  int guard = 0;                  // fill-vs-walk guard: times this pair was re-run because its walk disagreed
 };
 
 }  // namespace
@@ -171,6 +172,8 @@ struct nwk_ctx {
   DevBuf d_work;                // matrices | boundary granules | op strings
   int64_t clean_b = 0;          // leading bytes of d_work holding only zeros / old-epoch granules
   DevBuf d_pairs, d_tasks, d_ctl, d_oplen, d_endij, d_done, d_stamps, d_prog, d_retry;
+  DevBuf d_endv;                // fill-vs-walk guard: per slot, the fill's H(m, n) (FillArgs::endv)
+  HostBuf h_endv[2];
   DevBuf d_segctl;              // kPacked2: task-done flags | segment info | traceback records; kCol: segment records
   DevBuf d_colinfo;             // kCol: segment info (int4 per segment), cleared per batch
   int64_t colseg_clean_b = 0;   // kCol: leading bytes of d_segctl holding only zeros / kCol records of older epochs
@@ -234,6 +237,7 @@ void nwk_ctx_destroy(nwk_ctx* c) {
   c->d_pairs.release(); c->d_tasks.release(); c->d_ctl.release();
   c->d_oplen.release(); c->d_endij.release(); c->d_done.release(); c->d_stamps.release(); c->d_retry.release();
   c->h_retry.release();
+  c->d_endv.release(); c->h_endv[0].release(); c->h_endv[1].release();
   c->d_segctl.release(); c->d_colinfo.release(); c->d_prog.release(); c->d_pen.release(); c->d_hash.release(); c->d_hq.release();
   for (auto& b : c->d_msa) b.release();
   for (int b = 0; b < 2; ++b) { c->h_pen[b].release(); c->h_hash[b].release(); c->h_rec[b].release(); }
@@ -833,6 +837,57 @@ struct FusedSync {
   int64_t missing = 0;
 };
 
+// Fill-vs-walk guard (skel:274: the reference's penalty IS the fill's
+// dp[m][n]).  The fill kernels below give their H(m, n) per pair
+// (FillArgs::endv); every finalize compares it with the cost of the walked
+// path, which equals it for a correct walk (the path telescopes to dp[m][n])
+// and exceeds it when the walk read a wrong code.  A pair that disagrees is
+// never published: it re-runs with full storage, and a second disagreement
+// fails the call with NWK_EKERNEL.
+bool guard_mode(int mode) {
+  return mode == kCol || mode == kBits || mode == kGotoh || mode == kAffinePk || mode == kAffine || mode == kPacked ||
+         mode == kPacked2 ||
+         mode == kProfile || mode == kCompare || mode == kLiteral;
+}
+
+struct GuardLog {
+  struct Bad {
+    int64_t idx;  // dp index
+    int endv, cost;
+  };
+  std::mutex mu;
+  std::vector<Bad> bad;
+  void add(int64_t idx, int endv, int cost) {
+    std::lock_guard<std::mutex> g(mu);
+    bad.push_back({idx, endv, cost});
+  }
+  std::vector<Bad> take() {
+    std::lock_guard<std::mutex> g(mu);
+    std::vector<Bad> r;
+    r.swap(bad);
+    return r;
+  }
+};
+
+// A pair whose walk disagreed with its fill (cost INT_MIN: computed on the
+// device, not copied back).  A path never costs less than the DP minimum, so
+// a cost below H(m, n) convicts the fill; above it, the walk read a wrong code
+// (or the fill's minimum is too low).
+int guard_rerun(const nwk_ctx* c, PairWork* w, int endv, int cost, nwk_stats* st) {
+  const char* who = cost == INT_MIN ? "the walk or the fill"
+                    : cost < endv   ? "the fill (a valid path costs less than its H(m, n))"
+                                    : "the walk (a wrong code read), or the fill";
+  if (w->guard >= 1)
+    return fail(NWK_EKERNEL, "pair %lld (%d x %d): the walked path's cost %d differs from the fill's H(m, n) = %d "
+                "again after a full-storage re-run: %s is wrong", (long long)w->id, w->m, w->n, cost, endv, who);
+  if (c->opts.verbose || getenv("NWK_GUARD_LOG"))
+    fprintf(stderr, "nwk guard: pair %lld (%d x %d, window %d): walked path cost %d, fill H(m, n) %d -> %s; re-run "
+            "with full storage\n", (long long)w->id, w->m, w->n, w->bits_w, cost, endv, who);
+  w->guard += 1;
+  st->guard_reruns += 1;
+  return NWK_OK;
+}
+
 struct Chain {
   const uint8_t* hashes = nullptr;  // [P][64] raw problem hashes
   std::vector<char> ready;
@@ -1017,7 +1072,20 @@ int align_linear_batch(nwk_ctx* c, const Plan& pl0, const Scoring& sc, const Pai
   };
   for (int q = 0; q < np; ++q)
     for (int b = 0; b < geo[q].nb; ++b) tk.push_back(make_int2(q, b));
+  // fill-vs-walk guard: pass 1 fills every cell and gives each pair's H(m, n)
+  static const int guard_env = getenv("NWK_GUARD") ? atoi(getenv("NWK_GUARD")) : 1;
+  std::vector<int> endv((size_t)np, 0);
+  if (guard_env != 0) {
+    if ((rc = c->d_endv.ensure(sizeof(int) * np)) != NWK_OK) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_endv.p, 0, sizeof(int) * np, c->stream));
+    fa.endv = c->d_endv.as<int>();
+    fa.pgap = sc.pgap;
+  }
   if ((rc = launch(1, &st->fill_ms)) != NWK_OK) return rc;
+  if (guard_env != 0) {
+    HIP_TRY(hipMemcpy(endv.data(), fa.endv, sizeof(int) * np, hipMemcpyDeviceToHost));
+    st->guard_checked += np;
+  }
   std::vector<int> ci((size_t)np), cj((size_t)np);
   std::vector<int64_t> off((size_t)np, 0);
   std::vector<std::vector<std::pair<int64_t, int>>> pieces((size_t)np);
@@ -1063,6 +1131,13 @@ int align_linear_batch(nwk_ctx* c, const Plan& pl0, const Scoring& sc, const Pai
     finalize_pair(c->seqs.data() + c->off[ws[q].i], ws[q].m, c->seqs.data() + c->off[ws[q].j], ws[q].n, sc, rev.data(),
                   (int)rev.size(), ci[q], cj[q], &outs[q], a1, a2);
   });
+  // the linear-space walk recomputes its bands from the same boundary rows, so
+  // a re-run would repeat a disagreement: it fails the call
+  if (guard_env != 0)
+    for (int q = 0; q < np; ++q)
+      if (outs[q].penalty != endv[q])
+        return fail(NWK_EKERNEL, "linear-space pair %lld (%d x %d): the walked path costs %d but the fill's H(m, n) is %d",
+                    (long long)ws[q].id, ws[q].m, ws[q].n, outs[q].penalty, endv[q]);
   for (int q = 0; q < np; ++q) st->matrix_bytes += geo[q].scratch_dw * 4;
   st->linear_space_pairs += np;
   st->batches += 1;
@@ -1377,9 +1452,47 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
   const bool dev_ok = a1 == nullptr && !c->has_us && fin_mode != 0;
   if (dev_ok && !dp.empty() && (rc = build_encoding(c, 1)) != NWK_OK) return rc;
   size_t pos = 0;
+  // a pair re-runs in a later batch: with full storage (windowed storage whose
+  // walk left the window, or a walk the fill-vs-walk guard rejected); the
+  // affine path has no linear-space fallback, so there it takes the widest
+  // doubled window that fits the budget when full storage does not
+  auto requeue = [&](PairWork w) -> int {
+    const int old_w = w.bits_w;
+    w.bits_w = 0;
+    footprint(&w, pl.bits, pl.mode, sc.affine, ggran);
+    auto need = [](const PairWork& x) {
+      return x.mat_dw * 4 + x.bnd_gr * 8 + 3 * x.ops_b + x.segops_b + x.segctl_b + 8192;
+    };
+    if ((pl.mode == kAffinePk || gotoh) && need(w) > c->budget) {
+      int nw = 0;
+      for (int64_t cw = 2 * (int64_t)std::max(old_w, 1); cw < (1 << 30); cw *= 2) {
+        PairWork t = w;
+        t.bits_w = (int)cw;
+        footprint(&t, pl.bits, pl.mode, sc.affine, ggran);
+        if (need(t) > c->budget) break;
+        nw = (int)cw;
+        if (t.mat_dw >= w.mat_dw) break;  // as wide as full storage
+      }
+      if (nw == 0)
+        return fail(NWK_ENOMEM, "pair %lld (%d x %d): its traceback left the %d-column storage window and "
+                    "neither full storage (%lld B) nor a %d-column window fits the HBM budget %lld",
+                    (long long)w.id, w.m, w.n, old_w, (long long)need(w), 2 * old_w, (long long)c->budget);
+      w.bits_w = nw;
+      footprint(&w, pl.bits, pl.mode, sc.affine, ggran);
+    }
+    if (dp.size() == dp.capacity())  // the async finalize holds pointers into dp
+      return fail(NWK_ENOMEM, "pair %lld: too many re-runs", (long long)w.id);
+    dp.push_back(w);
+    return NWK_OK;
+  };
+  // fill-vs-walk guard mismatches found by the host finalize threads (dp index, H(m, n), path cost)
+  GuardLog gl;
+  static const int guard_env = getenv("NWK_GUARD") ? atoi(getenv("NWK_GUARD")) : 1;
+  const bool guard_on = guard_env != 0;
   std::vector<std::shared_ptr<FusedSync>> fused_all;  // streamed batches (checked after the last join)
   double h_setup = 0, h_sync = 0, h_join = 0, h_last = 0;  // host phases (verbose)
   const bool lin_all = c->opts.linear_space > 0 && !sc.affine;  // (tests: every pair through f2)
+  for (;;) {
   while (pos < dp.size()) {
     // ---- form a batch that fits the HBM budget
     size_t end = pos;
@@ -1485,6 +1598,12 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       HIP_TRY(hipMemsetAsync(c->d_work.as<uint8_t>() + c->clean_b, 0, (size_t)(bnd_need_b - c->clean_b), c->stream));
     }
     c->clean_b = bnd_need_b;
+    // debug: NWK_POISON_BATCH=<byte> fills this batch's matrix region before the
+    // launch, so a walk reading a cell no band of this batch wrote reads that byte
+    // (for nw_align_pka 0x22 is tag 2, a code the fill never writes: the walk fails)
+    static const int poison_batch = getenv("NWK_POISON_BATCH") ? atoi(getenv("NWK_POISON_BATCH")) : -1;
+    if (poison_batch >= 0 && mat > 0)
+      HIP_TRY(hipMemsetAsync(c->d_work.as<uint8_t>() + mat_base_b, poison_batch & 0xff, (size_t)mat * 4, c->stream));
     // ---- descriptors and dependency-ordered band tasks (band-major)
     const int par = st.batches & 1;  // host buffer set of this batch
     if ((rc = c->h_pairs[par].ensure(sizeof(PairDesc) * np)) != NWK_OK) return rc;
@@ -1611,7 +1730,16 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipMemsetAsync(c->d_done.p, 0, sizeof(unsigned) * np, c->stream));
     bool windowed = false;
     for (int q = 0; q < np && !windowed; ++q) windowed = pd[q].bits_w > 0;
-    if (windowed) HIP_TRY(hipMemsetAsync(c->d_retry.p, 0, sizeof(int) * np, c->stream));
+    // fill-vs-walk guard (skel:274): the kernels that give their H(m, n) per
+    // pair (FillArgs::endv); NWK_GUARD=0 disables (A/B)
+    const bool guard = guard_on && guard_mode(pl.mode) && !(getenv("NWK_AFF_NOTRACE") || getenv("NWK_NOTRACE"));
+    if (guard) {
+      st.guard_checked += np;
+      if ((rc = c->d_endv.ensure(sizeof(int) * np)) != NWK_OK) return rc;
+      if ((rc = c->h_endv[par].ensure(sizeof(int) * np)) != NWK_OK) return rc;
+      HIP_TRY(hipMemsetAsync(c->d_endv.p, 0, sizeof(int) * np, c->stream));
+    }
+    if (windowed || guard) HIP_TRY(hipMemsetAsync(c->d_retry.p, 0, sizeof(int) * np, c->stream));
     // [tdone u32 | seginfo 8 x int | recs u64 | job ready u32 | head, tail | jobs int2]
     const int64_t seginfo_base_b = ntasks * 4;
     const int64_t rec_base_b = round_up(seginfo_base_b + nsegs * 32, 8);
@@ -1673,6 +1801,13 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.yw = bitsy || gotoh ? c->d_yw.as<unsigned>() : nullptr;
     fa.strip_ring = strip_ring;
     fa.retry = c->d_retry.as<int>();
+    fa.endv = guard ? c->d_endv.as<int>() : nullptr;
+    fa.pxy = sc.pxy;
+    fa.pgap = sc.pgap;
+    // (tests) NWK_DBG_CORRUPT = slot + 1: the first batch of the call (every batch with
+    // NWK_DBG_CORRUPT_ALL) flips the stored code of cell (m, n) of that pair before its walk
+    fa.dbg_corrupt = (st.batches == 0 || getenv("NWK_DBG_CORRUPT_ALL")) && getenv("NWK_DBG_CORRUPT")
+                         ? atoi(getenv("NWK_DBG_CORRUPT")) : 0;
     if (getenv("NWK_WATCHDOG")) {
       if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;
       HIP_TRY(hipMemsetAsync(c->d_prog.p, 0, 4 * (size_t)(grid + 1) * 4, c->stream));
@@ -1759,8 +1894,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     fa.host_rec = nullptr;
     if (hstream) {
       if ((rc = c->h_opsm[par].ensure((size_t)ops + 256, hipHostMallocMapped | hipHostMallocCoherent)) != NWK_OK) return rc;
-      if ((rc = c->h_hrec[par].ensure(16 * (size_t)np, hipHostMallocMapped | hipHostMallocCoherent)) != NWK_OK) return rc;
-      memset(c->h_hrec[par].p, 0, 16 * (size_t)np);
+      const size_t hrb = sizeof(int) * kHostRecInts * (size_t)np;
+      if ((rc = c->h_hrec[par].ensure(hrb, hipHostMallocMapped | hipHostMallocCoherent)) != NWK_OK) return rc;
+      memset(c->h_hrec[par].p, 0, hrb);
       void *dops = nullptr, *drec = nullptr;
       HIP_TRY(hipHostGetDevicePointer(&dops, c->h_opsm[par].p, 0));
       HIP_TRY(hipHostGetDevicePointer(&drec, c->h_hrec[par].p, 0));
@@ -1811,6 +1947,8 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       ha.gext = sc.affine ? sc.ge : sc.pgap;
       ha.penalties = c->d_pen.as<int>();
       ha.hashes = c->d_hash.as<uint8_t>();
+      ha.endv = fa.endv;
+      ha.retry = fa.retry;
       HIP_TRY(launch_hash(ha, c->stream));
     }
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
@@ -1875,10 +2013,13 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       const int* hrec = c->h_hrec[par].as<int>();
       const uint8_t* hops = c->h_opsm[par].as<uint8_t>();
       const int64_t obase = ops_base_b;
-      fin.start([c, np, dwf, pdh, fsync, ep, hrec, hops, obase, sc, penalties, hashes, chain]() {
+      GuardLog* glog = &gl;
+      const bool gchk = guard;
+      const int64_t gpos = (int64_t)pos;
+      fin.start([c, np, dwf, pdh, fsync, ep, hrec, hops, obase, sc, penalties, hashes, chain, glog, gchk, gpos]() {
         // state per pair: 0 pending, 1 claimed, 2 finalized, 3 left the window (re-run), 4 the
         // walk failed (length -2: the launch reports the error; the pair is never finalized,
-        // reported or chained)
+        // reported or chained), 5 its path's cost is not the fill's H(m, n) (guard: re-run)
         std::unique_ptr<std::atomic<int>[]> state(new std::atomic<int>[(size_t)np]);
         for (int64_t q = 0; q < np; ++q) state[q].store(0, std::memory_order_relaxed);
         std::atomic<int64_t> nleft{np};
@@ -1888,22 +2029,28 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
             if (d == 2 || nleft.load(std::memory_order_acquire) == 0) return;
             bool any = false;
             for (int64_t q = 0; q < np; ++q) {
-              if (state[q].load(std::memory_order_relaxed) != 0 || __atomic_load_n(hrec + 4 * q, __ATOMIC_ACQUIRE) != (int)ep)
+              const int* hr = hrec + kHostRecInts * q;
+              if (state[q].load(std::memory_order_relaxed) != 0 || __atomic_load_n(hr, __ATOMIC_ACQUIRE) != (int)ep)
                 continue;
               int z = 0;
               if (!state[q].compare_exchange_strong(z, 1)) continue;
               any = true;
-              const int len = hrec[4 * q + 1];
+              const int len = hr[1];
               if (len < 0) {
                 state[q].store(len == -1 ? 3 : 4, std::memory_order_release);
               } else {
                 const PairWork& w = dwf[q];
                 Finalized f;
                 finalize_pair(c->seqs.data() + c->off[w.i], w.m, c->seqs.data() + c->off[w.j], w.n, sc,
-                              hops + (pdh[q].ops_off - obase), len, hrec[4 * q + 2], hrec[4 * q + 3], &f);
-                penalties[w.out] = f.penalty;
-                memcpy(hashes + 64 * w.out, f.hash, 64);
-                state[q].store(2, std::memory_order_release);
+                              hops + (pdh[q].ops_off - obase), len, hr[2], hr[3], &f);
+                if (gchk && f.penalty != hr[4]) {
+                  glog->add(gpos + q, hr[4], f.penalty);
+                  state[q].store(5, std::memory_order_release);
+                } else {
+                  penalties[w.out] = f.penalty;
+                  memcpy(hashes + 64 * w.out, f.hash, 64);
+                  state[q].store(2, std::memory_order_release);
+                }
               }
               nleft.fetch_sub(1, std::memory_order_acq_rel);
             }
@@ -1931,7 +2078,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
             told[(size_t)q] = 1;
             any = true;
           }
-          while (lo < np && (told[(size_t)lo] || state[lo].load(std::memory_order_acquire) == 3)) ++lo;
+          while (lo < np && (told[(size_t)lo] || state[lo].load(std::memory_order_acquire) == 3 ||
+                             state[lo].load(std::memory_order_acquire) == 5))
+            ++lo;
           if (chain && any) chain->advance();
         };
         std::thread rep_thread;
@@ -1953,7 +2102,7 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         for (int64_t q = 0; q < np; ++q) {
           const int st_q = state[q].load();
           const bool skipped = !fsync->skip.empty() && fsync->skip[(size_t)q];
-          if ((st_q != 2 && !skipped) || (st_q == 2 && skipped)) ++fsync->missing;
+          if ((st_q != 2 && st_q != 5 && !skipped) || (st_q == 2 && skipped)) ++fsync->missing;
         }
       });
     }
@@ -1982,7 +2131,9 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     HIP_TRY(hipMemcpyAsync(&herr, fa.err, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_oplen[par].p, fa.oplen, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_endij[par].p, fa.endij, sizeof(int2) * np, hipMemcpyDeviceToHost, c->stream));
-    if (windowed) HIP_TRY(hipMemcpyAsync(c->h_retry.p, fa.retry, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
+    if (windowed || guard)
+      HIP_TRY(hipMemcpyAsync(c->h_retry.p, fa.retry, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
+    if (guard) HIP_TRY(hipMemcpyAsync(c->h_endv[par].p, fa.endv, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
     if (fuse) {
       // records arrive in host memory on their own
     } else if (devhash) {  // 68 bytes per pair instead of the move strings
@@ -2090,42 +2241,21 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     // kBits windowed storage: pairs whose path left the window get no result
     // from this batch; they re-run with full storage in a later batch
     std::vector<char> skip;
-    if (windowed) {
+    if (windowed || guard) {
       const int* rt = c->h_retry.as<int>();
       for (int q = 0; q < np; ++q) {
         if (!rt[q]) continue;
         if (skip.empty()) skip.assign((size_t)np, 0);
         skip[q] = 1;
         PairWork w = dp[pos + q];
-        const int old_w = w.bits_w;
-        w.bits_w = 0;
-        footprint(&w, pl.bits, pl.mode, sc.affine, ggran);
-        auto need = [](const PairWork& x) {
-          return x.mat_dw * 4 + x.bnd_gr * 8 + 3 * x.ops_b + x.segops_b + x.segctl_b + 8192;
-        };
-        if ((pl.mode == kAffinePk || gotoh) && need(w) > c->budget) {
-          // the affine path has no linear-space fallback: re-run with the
-          // widest doubled window that fits the budget instead of in full
-          int nw = 0;
-          for (int64_t cw = 2 * (int64_t)old_w; cw < (1 << 30); cw *= 2) {
-            PairWork t = w;
-            t.bits_w = (int)cw;
-            footprint(&t, pl.bits, pl.mode, sc.affine, ggran);
-            if (need(t) > c->budget) break;
-            nw = (int)cw;
-            if (t.mat_dw >= w.mat_dw) break;  // as wide as full storage
-          }
-          if (nw == 0)
-            return fail(NWK_ENOMEM, "pair %lld (%d x %d): its traceback left the %d-column storage window and "
-                        "neither full storage (%lld B) nor a %d-column window fits the HBM budget %lld",
-                        (long long)w.id, w.m, w.n, old_w, (long long)need(w), 2 * old_w, (long long)c->budget);
-          w.bits_w = nw;
-          footprint(&w, pl.bits, pl.mode, sc.affine, ggran);
+        if (rt[q] == 2) {  // the guard, on the device (nw_rows / the fused finalize)
+          const int ev = c->h_endv[par].as<int>()[q];
+          const int pw = devhash && !fuse ? c->h_pen[par].as<int>()[q] : INT_MIN;  // (fused: on the device only)
+          if ((rc = guard_rerun(c, &w, ev, pw, &st)) != NWK_OK) return rc;
+        } else {
+          st.window_retries += 1;
         }
-        if (dp.size() == dp.capacity())  // the async finalize holds pointers into dp
-          return fail(NWK_ENOMEM, "pair %lld: too many window re-runs", (long long)w.id);
-        dp.push_back(w);
-        st.window_retries += 1;
+        if ((rc = requeue(w)) != NWK_OK) return rc;
       }
     }
     if (fuse || hstream) {  // the consumer finishes on its own; the next join collects it
@@ -2154,8 +2284,13 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     const PairWork* dw = dp.data() + pos;
     const int* hpen = c->h_pen[par].as<int>();
     const uint8_t* hhash = c->h_hash[par].as<uint8_t>();
+    const int* hev = guard ? c->h_endv[par].as<int>() : nullptr;  // the fill's H(m, n) per slot
+    GuardLog* glog = &gl;
+    const int64_t gpos = (int64_t)pos;
     auto job = [c, a1, a2, np, dw, pd, ol, ej, hops, ops_base_b, sc, penalties, hashes, chain, devhash, hpen, hhash,
-                skip]() {
+                skip, hev, glog, gpos]() mutable {
+      // (guard: pairs whose walked path does not cost the fill's H(m, n) join the skipped ones and re-run)
+      if (hev && !devhash && skip.empty()) skip.assign((size_t)np, 0);
       auto skipped = [&](int64_t q) { return !skip.empty() && skip[(size_t)q]; };
       if (devhash) {
         for (int64_t q = 0; q < np; ++q) {
@@ -2170,6 +2305,11 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
         Finalized f;
         finalize_pair(c->seqs.data() + c->off[w.i], w.m, c->seqs.data() + c->off[w.j], w.n, sc,
                       hops + (d.ops_off - ops_base_b), ol[q], ej[q].x, ej[q].y, &f, a1, a2);
+        if (hev && f.penalty != hev[q]) {
+          glog->add(gpos + q, hev[q], f.penalty);
+          skip[(size_t)q] = 1;  // (one thread per q: no other writer of this byte)
+          return;
+        }
         penalties[w.out] = f.penalty;
         memcpy(hashes + 64 * w.out, f.hash, 64);
       });
@@ -2192,6 +2332,15 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     pos = end;
   }
   fin.join();
+  // pairs the host finalize rejected (fill-vs-walk guard) re-run in new batches
+  const auto gbad = gl.take();
+  if (gbad.empty()) break;
+  for (const auto& g : gbad) {
+    PairWork w = dp[(size_t)g.idx];
+    if ((rc = guard_rerun(c, &w, g.endv, g.cost, &st)) != NWK_OK) return rc;
+    if ((rc = requeue(w)) != NWK_OK) return rc;
+  }
+  }
   for (const auto& f : fused_all)
     if (f->missing) return fail(NWK_EKERNEL, "fused finalize: %lld pair(s) without a record", (long long)f->missing);
   st.total_ms = now_ms() - t_start;
@@ -3060,6 +3209,13 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
     fa.prow = d_prow.as<int>();
     fa.pcol = d_pcol.as<int>();
     fa.lin_mode = dot;  // the profile packing: nw_profile<5 | 4 | 2 | 0> (launch_fill)
+    // fill-vs-walk guard: each merge's H(m, n) against the cost of its walked path (below)
+    static const int msa_guard = getenv("NWK_GUARD") ? atoi(getenv("NWK_GUARD")) : 1;
+    if (msa_guard != 0) {
+      if ((rc = c->d_endv.ensure(sizeof(int) * np)) != NWK_OK) return rc;
+      HIP_TRY(hipMemsetAsync(c->d_endv.p, 0, sizeof(int) * np, c->stream));
+      fa.endv = c->d_endv.as<int>();
+    }
     const int grid = (int)std::min<int64_t>(fill_blocks_per_cu(kProfileDP, 4) * c->cus, ceil_div(ntasks, 4));
     if (getenv("NWK_WATCHDOG")) {
       if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;
@@ -3083,8 +3239,10 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
     std::vector<int> ol((size_t)np);
     std::vector<int2> ej((size_t)np);
     std::vector<uint8_t> hops((size_t)ops);
+    std::vector<int> mev((size_t)np, 0);
     unsigned herr = 0;
     HIP_TRY(hipMemcpyAsync(&herr, fa.err, 4, hipMemcpyDeviceToHost, c->stream));
+    if (fa.endv) HIP_TRY(hipMemcpyAsync(mev.data(), fa.endv, 4 * (size_t)np, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(ol.data(), fa.oplen, 4 * np, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(ej.data(), fa.endij, 8 * np, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(hops.data(), d_mw.as<uint8_t>() + bnd_b + mat_b, (size_t)ops, hipMemcpyDeviceToHost, c->stream));
@@ -3162,6 +3320,13 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
         j += m != 'U';
       }
       if (i != X.len || j != Y.len) return fail(NWK_EKERNEL, "nwk_msa: traced path ends at (%d, %d) of (%d, %d)", i, j, X.len, Y.len);
+      // the merge's walked path must cost the fill's H(m, n) (skel:274's ret = dp[m][n])
+      if (fa.endv) {
+        ++st.guard_checked;
+        if (cost != (int64_t)mev[(size_t)q])
+          return fail(NWK_EKERNEL, "nwk_msa: merge %d x %d: the walked path costs %lld but the fill's H(m, n) is %d",
+                      X.len, Y.len, (long long)cost, mev[(size_t)q]);
+      }
       *sop += cost;
       std::vector<int>().swap(Xm.cnt);
       std::vector<int>().swap(Ym.cnt);

@@ -53,7 +53,8 @@ class Stats(ctypes.Structure):
                 ("bits", ctypes.c_int32), ("mode", ctypes.c_int32),
                 ("fill_launches", ctypes.c_int32), ("device_finalized", ctypes.c_int32),
                 ("linear_space_pairs", ctypes.c_int32), ("window_retries", ctypes.c_int32),
-                ("window", ctypes.c_int32)]
+                ("window", ctypes.c_int32), ("guard_checked", ctypes.c_int32),
+                ("guard_reruns", ctypes.c_int32)]
 
 
 # Every exported symbol of include/nwk.h with its ctypes signature.

@@ -194,8 +194,55 @@ def job_c5_scores():
                                  "affine variant has no reference, SURVEY §8 a9)"})
 
 
+def _c5_affine_pair(args):
+    p, x, y, pxy, go, ge = args
+    return p, oracle.score_affine(x, y, pxy, go, ge)
+
+
+def job_c5_pen(procs=6):
+    """All 496 C5 affine penalties (go=3, ge=1) from the oracle's O(n)-memory
+    Gotoh scorer (nwo_score_affine), pair-parallel, checkpointed to
+    /tmp/c5_pen.jsonl so an interrupted run resumes.  ~2e13 cells: ~1.5-2 h on
+    6 processes here.  bench.py --workload c5 checks every penalty of its last
+    timed step against this file."""
+    from multiprocessing import Pool
+    desc, k, L, pxy, pgap, (go, ge) = workloads.SYNTH["c5"]
+    genes = workloads.synth(k, L)
+    P = k * (k - 1) // 2
+    ck = "/tmp/c5_pen.jsonl"
+    done = {}
+    if os.path.exists(ck):
+        for line in open(ck):
+            r = json.loads(line)
+            done[r[0]] = r[1]
+    todo, p = [], 0
+    for i in range(1, k):
+        for j in range(i):
+            if p not in done:
+                todo.append((p, genes[i], genes[j], pxy, go, ge))
+            p += 1
+    t0 = time.time()
+    with Pool(procs) as pool, open(ck, "a") as f:
+        for p, pen in pool.imap_unordered(_c5_affine_pair, todo, chunksize=1):
+            done[p] = pen
+            f.write(json.dumps([p, pen]) + "\n")
+            f.flush()
+            print("c5_pen: %d/%d pairs, %.0f s" % (len(done), P, time.time() - t0), file=sys.stderr)
+    pens = [done[p] for p in range(P)]
+    ref = json.load(open(os.path.join(OUT, "c5_scores.json")))
+    for s in ref["scores"]:
+        p = s["i"] * (s["i"] - 1) // 2 + s["j"]
+        assert pens[p] == s["affine_penalty"], "c5_pen disagrees with c5_scores.json"
+    save("c5_pen", {"config": desc, "k": k, "L": L, "pxy": pxy, "go": go, "ge": ge, "penalties": pens,
+                    "source": "oracle nwo_score_affine (O(n)-memory Gotoh restatement; the affine variant "
+                              "has no reference, SURVEY §8 a9), %d processes, %.0f s" % (procs, time.time() - t0)})
+
+
 def main(argv):
     for a in argv or ["c3", "c3_pairs", "c4", "c4_pairs", "edge16", "c5_scores"]:
+        if a == "c5_pen":
+            job_c5_pen()
+            continue
         if a in ("c3", "c4"):
             job_full(a)
         elif a in ("c3_oracle", "c4_oracle"):
