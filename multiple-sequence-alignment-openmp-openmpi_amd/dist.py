@@ -408,6 +408,14 @@ class NodeRecords:
         nonce = int(comm.max(float(nonce)))  # rank 0's nonce (< 2^53), after it created the segment
         if self.rank != 0:
             self.shm = shared_memory.SharedMemory(name=self.name)
+            # Python < 3.13 registers an attached segment with this process's
+            # resource tracker, which would unlink it (and warn) when a peer
+            # exits: only rank 0 owns the segment's lifetime
+            try:
+                from multiprocessing import resource_tracker
+                resource_tracker.unregister(self.shm._name, "shared_memory")
+            except Exception:
+                pass
             if int(np.ndarray((1,), dtype=np.int64, buffer=self.shm.buf)[0]) != nonce:
                 raise RuntimeError("rank %d: node record segment %s is not this run's" % (self.rank, self.name))
         self.flags = np.ndarray((self.world, chunks), dtype=np.int64, buffer=self.shm.buf, offset=64)
@@ -429,8 +437,14 @@ class NodeRecords:
         return self.data[:, self.pre[c]:self.pre[c + 1]].reshape(-1, REC).copy()
 
     def shard_blocks(self):
-        """Every rank's whole padded shard (rank-major), as this rank published it."""
+        """Every rank's whole padded shard (rank-major), as it is in the segment NOW
+        (a peer that has returned may already publish its next call's pieces)."""
         return self.data.reshape(-1, REC)
+
+    def as_shards(self, taken):
+        """The pieces wait() returned, in piece order, rearranged rank-major over
+        whole shards -- the layout of the all-gather of every rank's shard."""
+        return np.concatenate([t.reshape(self.world, -1, REC) for t in taken], axis=1).reshape(-1, REC)
 
     def close(self):
         shm, self.shm = getattr(self, "shm", None), None
@@ -439,6 +453,14 @@ class NodeRecords:
         self.flags = self.data = None
         shm.close()
         if self.rank == 0:
+            try:
+                # (ranks spawned by one parent share its resource tracker, where a
+                # peer's unregister above removed the name: re-register it so the
+                # unregister inside unlink() finds it)
+                from multiprocessing import resource_tracker
+                resource_tracker.register(shm._name, "shared_memory")
+            except Exception:
+                pass
             try:
                 shm.unlink()
             except FileNotFoundError:
@@ -529,6 +551,7 @@ def _exchange_node(shard, chunks, rank, P, comm, node, token):
     chain = seqalign.ChainStream(P) if rank == 0 else None
     err = None
     blocks = []
+    taken = []  # rank 0: the pieces the chain took (copies: peers reuse the segment once they return)
     try:
         shard.start()
         for c in range(chunks):
@@ -537,8 +560,10 @@ def _exchange_node(shard, chunks, rank, P, comm, node, token):
             node.publish(c, b, token)
             if chain is None or err is not None:
                 continue
+            got = node.wait(c, token)
+            taken.append(got)
             try:
-                cid, cpen, chs = unpack_chunk(node.wait(c, token))
+                cid, cpen, chs = unpack_chunk(got)
             except RankFailed as e:
                 err = e
                 continue
@@ -553,7 +578,9 @@ def _exchange_node(shard, chunks, rank, P, comm, node, token):
             raise RankFailed("rank %d: %s" % (rank, err)) from err
         if chain is None:
             return None, None, None
-        if not np.array_equal(np.asarray(g, dtype=np.uint8).reshape(-1, REC), node.shard_blocks()):
+        # (against the copies taken: after the last collective a peer may already
+        # publish its next call's pieces into the live segment)
+        if not np.array_equal(np.asarray(g, dtype=np.uint8).reshape(-1, REC), node.as_shards(taken)):
             raise RuntimeError("rank 0: the all-gathered records differ from the node records the chain took")
         return chain.finish()
     finally:

@@ -265,7 +265,7 @@ class _OracleStreamEngine(_OracleEngine):
         return self._pen, self._hs
 
 
-def _streamed_worker(rank, world, port, cases, chunks, fail, q, node_records=False, steps=1):
+def _streamed_worker(rank, world, port, cases, chunks, fail, q, node_records=False, steps=1, scorings=None):
     import sys
 
     for p in (PKG, ORACLE):
@@ -284,10 +284,12 @@ def _streamed_worker(rank, world, port, cases, chunks, fail, q, node_records=Fal
             try:
                 for step in range(1, steps + 1):  # (the segment is reused across steps: token = step)
                     eng = _OracleStreamEngine(genes, fail_end=fail and rank == world - 1)
+                    sp, sg = scorings[step - 1] if scorings else (pxy, pgap)
                     try:
-                        h, pen, _ = nwdist.align_sharded_streamed(eng, lens, pxy, pgap, rank, world, chunks=chunks,
+                        h, pen, _ = nwdist.align_sharded_streamed(eng, lens, sp, sg, rank, world, chunks=chunks,
                                                                   poll_s=0.0, node=node, token=step)
-                        q.put((rank, name, h, None if pen is None else [int(v) for v in pen]))
+                        q.put((rank, "%s@%d,%d" % (name, sp, sg) if scorings else name, h,
+                               None if pen is None else [int(v) for v in pen]))
                     except nwdist.RankFailed as e:
                         q.put((rank, name, "raised: %s" % e, None))
             finally:
@@ -326,6 +328,41 @@ def test_gloo_streamed_pieces_match_golden(world, chunks, node):
         if rank == 0:
             assert h == gold[name]["hash"], name
             assert pen == gold[name]["penalties"], name
+        else:
+            assert h is None
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_node_records_consecutive_calls_different_scorings(world):
+    """consecutive streamed calls with DIFFERENT records on one
+    NodeRecords segment.  A peer that has returned publishes its next call's
+    pieces into the live segment while rank 0 may still be checking the last
+    all-gather -- rank 0 compares against the copies its chain took, so every
+    call's hash equals the oracle's for its own scoring."""
+    import oracle
+
+    c = CASES[0]
+    _, _, genes = case_input(c)
+    scorings = [(3, 2), (5, 1), (1, 1), (3, 2)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    cases = [(c["name"], 0, 0, genes)]
+    procs = [ctx.Process(target=_streamed_worker, args=(r, world, port, cases, 3, False, q, True, len(scorings),
+                                                       scorings)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world * len(scorings))]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = {}
+    for sp, sg in scorings:
+        h, pen, _ = oracle.all_pairs(genes, sp, sg)
+        want["%s@%d,%d" % (c["name"], sp, sg)] = (h, pen)
+    for rank, name, h, pen in out:
+        if rank == 0:
+            assert (h, pen) == want[name], name
         else:
             assert h is None
 
