@@ -81,6 +81,13 @@ def load_workload(name):
         if os.path.exists(f) and affine is None:
             g = json.load(open(f))
             expect = {"hash": g["hash"], "penalties": g["penalties"], "source": g["source"]}
+        fa = os.path.join(GOLDEN, "large", name + "_pen.json")
+        if affine is not None and os.path.exists(fa):
+            # the affine variant has no reference: every penalty
+            # against the oracle's O(n)-memory Gotoh scorer, no answer hash
+            g = json.load(open(fa))
+            expect = {"hash": None, "penalties": g["penalties"], "source": g["source"],
+                      "affine": (g["go"], g["ge"])}
         return desc, pxy, pgap, workloads.synth(k, L), affine, expect
     raise SystemExit("unknown workload " + name)
 
@@ -422,8 +429,10 @@ def main():
     name, pxy, pgap, genes, affine, expect = load_workload(args.workload)
     if args.affine is not None:
         affine = tuple(int(v) for v in args.affine.split(","))
-    if affine and tuple(affine) != (0, pgap):
+    if affine and tuple(affine) != (0, pgap) and (expect is None or tuple(expect.get("affine", ())) != tuple(affine)):
         expect = None  # the reference's answers are for linear gaps (== affine go=0, ge=pgap only)
+    elif affine and expect is not None and "affine" in expect and tuple(affine) == (0, pgap):
+        expect = None  # (an affine fixture's penalties are not the linear run's)
     if affine:
         go, ge = affine
     k = len(genes)
@@ -456,9 +465,17 @@ def main():
     # RCCL kernel cannot start while the persistent fill holds every SIMD's
     # registers: dist.NodeRecords).  NWK_NODE_RECORDS=0: one
     # all-gather per piece instead.
+    # Since round 6 the records go one at a time (NWK_BENCH_RECORDS=1, the
+    # default: dist.NodeStream, rank 0's chain takes each record as soon as its
+    # rank has published it); NWK_BENCH_RECORDS=0 keeps the 16 pieces.
     node = None
+    per_record = False
     if stream and nwdist.node_local(world) and os.environ.get("NWK_NODE_RECORDS", "1") != "0":
-        node = nwdist.NodeRecords(comm, chunks, nwdist.chunk_parts(lengths, rank, world, chunks)[1])
+        per_record = os.environ.get("NWK_BENCH_RECORDS", "1") != "0"
+        if per_record:
+            node = nwdist.NodeStream(comm, nwdist.stream_per(lengths, world))
+        else:
+            node = nwdist.NodeRecords(comm, chunks, nwdist.chunk_parts(lengths, rank, world, chunks)[1])
     token = [0]
     piece_stats = []
     last_hs = [None]
@@ -469,7 +486,13 @@ def main():
         del piece_t[:]
         hs = None
         t_step = time.perf_counter()
-        if stream:
+        if per_record:
+            token[0] += 1
+            h, pen, hs = nwdist.align_sharded_records(
+                eng, lengths, pxy, pgap, rank, world, node, token[0], comm=comm,
+                on_first=lambda: piece_t.append(round((time.perf_counter() - t_step) * 1e3, 3)))
+            piece_stats.append(eng.stats())
+        elif stream:
             token[0] += 1
             h, pen, hs = nwdist.align_sharded_streamed(
                 eng, lengths, pxy, pgap, rank, world, chunks=chunks, comm=comm, node=node, token=token[0],
@@ -500,7 +523,7 @@ def main():
     def check(pen, h):
         if rank != 0 or expect is None:
             return None
-        return h == expect["hash"] and [int(v) for v in pen] == expect["penalties"]
+        return (expect["hash"] is None or h == expect["hash"]) and [int(v) for v in pen] == expect["penalties"]
 
     checks = []
     for _ in range(args.warmup):
@@ -562,10 +585,13 @@ def main():
                    "gaps": ("affine go=%d ge=%d" % (go, ge)) if affine else "linear pgap=%d" % pgap,
                    "storage_bits_per_cell": st["bits"], "mode": seqalign.MODES.get(st["mode"]),
                    "parallelism": "pair-sharded dp%d (LPT), %d all-gather(s) of 72-B records, chain streamed on rank 0%s" % (
-                       world, chunks if sharded and not affine else 1,
+                       world, chunks if sharded and not affine and node is None else 1,
                        "; one launch per rank, records streamed per pair (fused device finalize)" if stream else "")},
         "answer_hash_ok": answer_ok,
         "answer_source": expect["source"] if expect else None,
+        "answer_checked": None if expect is None else (
+            "all %d penalties (no reference hash for the affine variant)" % P if expect["hash"] is None
+            else "answer hash + all %d penalties" % P),
         "kernel": {"name": kernel, "fill_ms": round(fill_ms, 3), "traceback_ms": round(float(np.mean(traces)), 3),
                    "fill_gcups": round(my_cells / (fill_ms * 1e-3) / 1e9, 2),
                    "fill_launches_per_step": launches, "batches": sum(x["batches"] for x in piece_stats),
@@ -577,11 +603,15 @@ def main():
     if sharded:
         out["collective"] = {"backend": comm.backend,
                              "all_gathers_per_step": 1 if affine or node is not None else chunks,
-                             "piece_exchange": "node shared memory (dist.NodeRecords), then one all-gather"
+                             "piece_exchange": "every record through node shared memory as it is out "
+                                               "(dist.NodeStream), then one all-gather" if per_record else
+                                               "node shared memory (dist.NodeRecords), then one all-gather"
                                                if node is not None else "one all-gather per piece",
                              "record_bytes": 72, "forced_at_world_1": world == 1,
-                             "pieces_per_rank": 1 if affine else chunks,
-                             "piece_ready_ms": list(piece_t)}  # rank 0, last timed step
+                             "pieces_per_rank": "per record" if per_record else 1 if affine else chunks,
+                             # rank 0, last timed step: when its chain took the first record
+                             # (per record), or when each piece's records were ready
+                             ("first_record_ms" if per_record else "piece_ready_ms"): list(piece_t)}
     # which HIP runtime / RCCL this process bound (torch, when imported first,
     # brings its own libamdhip64 / librccl and libnwk.so binds to those)
     out["runtime_libs"] = mapped_libs()

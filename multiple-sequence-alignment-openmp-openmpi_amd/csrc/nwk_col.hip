@@ -132,14 +132,17 @@ __device__ __forceinline__ void col_hops(u64 (&c)[NP], unsigned (&acc)[NP], cons
 //   inj      the band above's last row for lane 0's columns of this half (bit q = column s_half + q)
 //   pub      CAP: acc after step s_half + 30's carries (columns s_half - 94 .. s_half - 63)
 //   MASK     steps of the first super-block: columns < 0 keep v = 0 (the left border)
-//   END      steps that may hold column capc = n - 1: the lane there adds the
-//            vertical differences of its rows (rowm: those < m) to cnt (the
-//            fill-vs-walk guard's end value, FillArgs::endv)
+//   END      steps that may hold column capc = n - 1: lane t = s - capc holds it;
+//            the scalar unit reads its vertical differences (v_readlane) and adds
+//            those of its rows < m (nvr0 - 32 t of them) to cnt (the fill-vs-walk
+//            guard's end value, FillArgs::endv).  All scalar: no VGPR lives
+//            across the loop for it (a per-lane mask and counter did, and the
+//            96-VGPR instantiation spilled ~270 registers: C3 145 -> 172 ms)
 template <int NP, int SR, bool MASK, bool CAP, int BLK, bool END>
 __device__ __forceinline__ void col_block(int s0, int lane, unsigned x0, unsigned x1, unsigned w0, unsigned w1,
                                           unsigned (&l)[NP], u64 (&c)[NP], unsigned (&acc)[NP],
                                           const u64 (&inj)[NP], unsigned (&pub)[NP], unsigned* st, bool sto,
-                                          int capc, unsigned rowm, int& cnt) {
+                                          int capc, int nvr0, int& cnt) {
   unsigned dw[8], uw[8];
   auto step = [&](auto qc) {
     constexpr int q = decltype(qc)::value;
@@ -167,9 +170,13 @@ __device__ __forceinline__ void col_block(int s0, int lane, unsigned x0, unsigne
 #pragma unroll
     for (int k = 0; k < NP; ++k) l[k] = Vn[k];
     if constexpr (END) {
-      const unsigned mk = s - lane == capc ? rowm : 0u;
+      const int t = s - capc;  // (uniform) the lane at column capc
+      if ((unsigned)t < 64u) {
+        const int nv = nvr0 - 32 * t;
+        const unsigned mk = nv >= 32 ? ~0u : (nv <= 0 ? 0u : (1u << nv) - 1u);
 #pragma unroll
-      for (int k = 0; k < NP; ++k) cnt += __builtin_popcount(Vn[k] & mk);
+        for (int k = 0; k < NP; ++k) cnt += __builtin_popcount((unsigned)__builtin_amdgcn_readlane((int)Vn[k], t) & mk);
+      }
     }
     if constexpr (SR < 0) dw[q] = match;
     else if constexpr (SR >= NP) dw[q] = ~0u;
@@ -1071,12 +1078,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const bool want_end = a.endv != nullptr;
     const int sbe = want_end ? (capc >> 6 > 1 ? capc >> 6 : 1) : nsb;
     const int capx = want_end ? capc : -1000;
-    int cnt = 0;
-    unsigned rowm = 0;
-    {
-      const int nvr = pd.m - R0 - 32 * lane;
-      rowm = nvr >= 32 ? ~0u : (nvr <= 0 ? 0u : (1u << nvr) - 1u);
-    }
+    int cnt = 0;                  // (uniform)
+    const int nvr0 = pd.m - R0;   // rows < m from lane 0's first row on
 
     auto half = [&](int h, auto mask_t, auto end_t) {
       constexpr bool MASK = decltype(mask_t)::value;
@@ -1116,7 +1119,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         // lane's words of it hold a cell within bits_w columns of the diagonal
         const bool sto = (unsigned)rel < (unsigned)nblk && (!win || bits_lane_stored(hi0 + (int64_t)s0 * pd.m, lim, hlim));
         unsigned* st = mb + (int64_t)rel * 1024;
-        col_block<NP, SR, MASK, B == 3, B, END>(s0, lane, x0, x1, wc0, wc1, l, c, acc, inj, pub, st, sto, capx, rowm,
+        col_block<NP, SR, MASK, B == 3, B, END>(s0, lane, x0, x1, wc0, wc1, l, c, acc, inj, pub, st, sto, capx, nvr0,
                                                 cnt);
       };
       blk(std::integral_constant<int, 0>{});
@@ -1153,8 +1156,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     BITS_PROG(0x30000000u);
     if (!ok) return;
     if (want_end) {  // this band's part of H(m, n): - sum v (+ (m + n) pgap once, band 0)
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
       if (lane == 0)
         __hip_atomic_fetch_add((gu32*)(a.endv + pd.slot), (unsigned)(band == 0 ? (pd.m + pd.n) * a.pgap - cnt : -cnt),
                                BITS_RLX);
@@ -1188,11 +1189,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #endif
       if (pd.bits_w > 0) trace_col<false, true>(a, pd, obuf_all[wid], pf_all[wid], lane, 0, tlen, tend, tout);
       else trace_col<false, false>(a, pd, obuf_all[wid], pf_all[wid], lane, 0, tlen, tend, tout);
-      __builtin_amdgcn_s_setprio(0);
       if constexpr (FUSE) {
+        // the first pieces of a streamed shard: rows, hash and record at once,
+        // still at the walk's priority (rank 0's chain waits for these records)
+        const bool early = a.early_hash > 0 && pd.prio >= a.early_hash;
+        if (!early) __builtin_amdgcn_s_setprio(0);
         const bool ok_rows = !tout && fin_rows(a, pd, lane, tlen, tend);
         hq_push(a, pd, lane, ok_rows);
+        if (early) hq_hash(a, lane, true);
       }
+      __builtin_amdgcn_s_setprio(0);
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
       BITS_PROG(0x56000000u);
     } else if (pd.spec_every > 0 && band + 1 < pd.nbands) {  // segmented: this band's speculative segment

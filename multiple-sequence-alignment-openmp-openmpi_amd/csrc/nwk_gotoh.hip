@@ -390,13 +390,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
     // fill-vs-walk guard: with v = G(i-1, j) - G(i, j) = VLO + (its planes set)
     // and G(0, n) = go, H(m, n) = go + (m + n) ge - sum_i v(i, n); row
     // 32 t + b reaches column n at step n + 32 t + b (segments kmax ..)
+    // At step s exactly one row of the band is at column n: band row r = s - n
+    // (lane r / 32, bit r % 32), so the scalar unit reads it (v_readlane) and
+    // no VGPR lives across the loop for the guard (a per-lane counter and row
+    // mask made the C5 instantiation spill 33 VGPRs)
     const int capn = a.endv ? pd.n : -100000;
-    int cnt = 0;  // planes set over this band's rows < m at column n
-    unsigned rowm;
-    {
-      const int nvr = pd.m - R0 - 32 * lane;
-      rowm = nvr >= 32 ? ~0u : (nvr <= 0 ? 0u : (1u << nvr) - 1u);
-    }
+    const int rows_m = pd.m - R0;  // band rows < m
+    int cnt = 0;                   // (uniform) planes set over this band's rows < m at column n
     for (int j = 0; j < nseg; ++j) {
       // --- the row above for lane 0's columns 32 j .. 32 j + 31 -> cons (bit 31 per column)
       {
@@ -472,11 +472,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
           step<C>(match, v, e, U, fU, vn, en, h, f, D, Fs, Ee, Fe);
 #pragma unroll
           for (int p = 0; p < NV; ++p) v[p] = vn[p];
-          if constexpr (END) {  // column n: bit s - n - 32 lane (rows < m)
-            const int bb = s - capn - 32 * lane;
-            const unsigned mk = (unsigned)bb < 32u ? (1u << bb) & rowm : 0u;
+          if constexpr (END) {  // column n: band row r = s - n (rows < m)
+            const int rr = s - capn;
+            if ((unsigned)rr < (unsigned)kBR && rr < rows_m) {
 #pragma unroll
-            for (int p = 0; p < NV; ++p) cnt += __builtin_popcount(vn[p] & mk);
+              for (int p = 0; p < NV; ++p)
+                cnt += (int)(((unsigned)__builtin_amdgcn_readlane((int)vn[p], rr >> 5) >> (rr & 31)) & 1u);
+            }
           }
 #pragma unroll
           for (int q = 0; q < NQ1; ++q) e[q] = en[q];
@@ -541,8 +543,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
     }
     if (!ok) return;
     if (a.endv) {  // this band's part of H(m, n) (+ the border terms once, band 0)
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
       const int rows = min(kBR, pd.m - R0);
       const int part = rows * GO - cnt + (band == 0 ? GO + (pd.m + pd.n) * GE : 0);
       if (lane == 0) __hip_atomic_fetch_add((gu32*)(a.endv + pd.slot), (unsigned)part, BITS_RLX);
