@@ -198,6 +198,10 @@ struct FillArgs {
   // publishing it.  nullptr: the kernel does not provide it.
   int* endv;
   int dbg_corrupt;         // debug (tests): slot + 1 whose stored code of cell (m, n) is flipped before its walk
+  // fused finalize of a streamed shard: a pair of PairDesc::prio >= early_hash
+  // (the first pieces of the canonical order) is hashed by its tracing wave at
+  // once instead of waiting for a group of 32 (0: off)
+  int early_hash;
 };
 // host_rec ints per slot: {flag, length, end i, end j, fill end value H(m, n), -, -, -}
 constexpr int kHostRecInts = 8;

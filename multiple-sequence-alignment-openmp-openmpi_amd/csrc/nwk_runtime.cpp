@@ -1808,6 +1808,12 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
     // NWK_DBG_CORRUPT_ALL) flips the stored code of cell (m, n) of that pair before its walk
     fa.dbg_corrupt = (st.batches == 0 || getenv("NWK_DBG_CORRUPT_ALL")) && getenv("NWK_DBG_CORRUPT")
                          ? atoi(getenv("NWK_DBG_CORRUPT")) : 0;
+    // streamed shards (finalize "fused" asked for): the first two pieces' pairs
+    // (prio >= 1 above) are hashed by their tracing wave at once, not in groups
+    // of 32 (the chain on rank 0 waits for the lowest canonical ids).
+    // NWK_EARLY_HASH=0 off, p > 0: prio >= p.
+    static const int early_env = getenv("NWK_EARLY_HASH") ? atoi(getenv("NWK_EARLY_HASH")) : 1;
+    fa.early_hash = c->opts.finalize == 3 ? early_env : 0;
     if (getenv("NWK_WATCHDOG")) {
       if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;
       HIP_TRY(hipMemsetAsync(c->d_prog.p, 0, 4 * (size_t)(grid + 1) * 4, c->stream));

@@ -368,28 +368,21 @@ class StreamedShard:
         return self.err
 
 
-class NodeRecords:
-    """Per-piece record blocks of every rank of one node, in POSIX shared
-    memory: rank r's block of piece c (per[c] records) at slot (r, c), then its
-    flag (int64) set to the step's token.  Stores are ordered by the x86-64
-    memory model (TSO, every MI355X host): a reader that sees the flag sees the
-    block.  Rank 0 creates the segment (a stale one of the same name is
-    replaced) and stamps it with a nonce that every rank receives through the
-    communicator before attaching, so no rank can read a segment left by an
-    earlier run."""
+class _NodeSegment:
+    """A POSIX shared-memory segment of one node's ranks, named by the run key:
+    rank 0 creates it (a stale one of the same name is replaced) and stamps it
+    with a nonce that every rank receives through the communicator before
+    attaching, so no rank can read a segment left by an earlier run.
+    layout(world) -> (header bytes after the nonce line, data bytes)."""
 
-    def __init__(self, comm, chunks, per, key=None):
+    def _open(self, comm, hdr_b, data_b, key=None):
         from multiprocessing import shared_memory
 
-        self.world, self.rank, self.chunks = comm.world, comm.rank, chunks
-        self.per = [int(x) for x in per]
-        self.pre = np.cumsum([0] + self.per)
-        self.sum_per = int(self.pre[-1])
+        self.world, self.rank = comm.world, comm.rank
         key = key or run_key()
-        self.name = "nwk_rec_%s" % key
-        flags_b = 8 * self.world * chunks
-        self.data_off = 64 + (flags_b + 63) // 64 * 64
-        size = self.data_off + self.world * self.sum_per * REC
+        self.name = "%s_%s" % (self.PREFIX, key)
+        self.data_off = 64 + (hdr_b + 63) // 64 * 64
+        size = self.data_off + max(int(data_b), 1)
         nonce = 0
         if self.rank == 0:
             try:  # a segment left by a run that died
@@ -402,7 +395,7 @@ class NodeRecords:
             # flags cleared BEFORE the nonce goes out: a peer may publish as soon
             # as it has it (clearing after the collective erased a fast peer's
             # first flag, and rank 0 waited for it forever)
-            np.ndarray((self.world, chunks), dtype=np.int64, buffer=self.shm.buf, offset=64)[:] = 0
+            np.ndarray((hdr_b // 8,), dtype=np.int64, buffer=self.shm.buf, offset=64)[:] = 0
             nonce = int.from_bytes(os.urandom(6), "little") | 1
             np.ndarray((1,), dtype=np.int64, buffer=self.shm.buf)[0] = nonce
         nonce = int(comm.max(float(nonce)))  # rank 0's nonce (< 2^53), after it created the segment
@@ -418,9 +411,49 @@ class NodeRecords:
                 pass
             if int(np.ndarray((1,), dtype=np.int64, buffer=self.shm.buf)[0]) != nonce:
                 raise RuntimeError("rank %d: node record segment %s is not this run's" % (self.rank, self.name))
+
+    def close(self):
+        shm, self.shm = getattr(self, "shm", None), None
+        if shm is None:
+            return
+        self._drop_views()
+        shm.close()
+        if self.rank == 0:
+            try:
+                # (ranks spawned by one parent share its resource tracker, where a
+                # peer's unregister above removed the name: re-register it so the
+                # unregister inside unlink() finds it)
+                from multiprocessing import resource_tracker
+                resource_tracker.register(shm._name, "shared_memory")
+            except Exception:
+                pass
+            try:
+                shm.unlink()
+            except FileNotFoundError:
+                pass
+
+
+class NodeRecords(_NodeSegment):
+    """Per-piece record blocks of every rank of one node, in POSIX shared
+    memory: rank r's block of piece c (per[c] records) at slot (r, c), then its
+    flag (int64) set to the step's token.  Stores are ordered by the x86-64
+    memory model (TSO, every MI355X host): a reader that sees the flag sees the
+    block.  Segment lifetime and nonce: _NodeSegment."""
+
+    PREFIX = "nwk_rec"
+
+    def __init__(self, comm, chunks, per, key=None):
+        self.chunks = chunks
+        self.per = [int(x) for x in per]
+        self.pre = np.cumsum([0] + self.per)
+        self.sum_per = int(self.pre[-1])
+        self._open(comm, 8 * comm.world * chunks, comm.world * self.sum_per * REC, key)
         self.flags = np.ndarray((self.world, chunks), dtype=np.int64, buffer=self.shm.buf, offset=64)
         self.data = np.ndarray((self.world, self.sum_per, REC), dtype=np.uint8, buffer=self.shm.buf,
                                offset=self.data_off)
+
+    def _drop_views(self):
+        self.flags = self.data = None
 
     def publish(self, c, block, token):
         """This rank's padded block of piece c, then its flag."""
@@ -446,25 +479,45 @@ class NodeRecords:
         whole shards -- the layout of the all-gather of every rank's shard."""
         return np.concatenate([t.reshape(self.world, -1, REC) for t in taken], axis=1).reshape(-1, REC)
 
-    def close(self):
-        shm, self.shm = getattr(self, "shm", None), None
-        if shm is None:
-            return
-        self.flags = self.data = None
-        shm.close()
-        if self.rank == 0:
-            try:
-                # (ranks spawned by one parent share its resource tracker, where a
-                # peer's unregister above removed the name: re-register it so the
-                # unregister inside unlink() finds it)
-                from multiprocessing import resource_tracker
-                resource_tracker.register(shm._name, "shared_memory")
-            except Exception:
-                pass
-            try:
-                shm.unlink()
-            except FileNotFoundError:
-                pass
+
+class NodeStream(_NodeSegment):
+    """Per-record exchange of one node's streamed ranks (round 6): rank r's
+    shard records at slots (r, 0 .. n_r) in its shard order (ascending
+    canonical ids), and one progress word per rank, on its own cache line:
+    token << 32 | records published so far (FAILED_COUNT: the rank failed),
+    stored after the records (x86-TSO: a reader that sees the count sees the
+    records).  Rank 0's chain takes each record as soon as its rank has
+    published it -- the master of sub:305-331 takes each worker's result as it
+    arrives -- instead of a piece of 1/16 of the canonical ids at a time."""
+
+    PREFIX = "nwk_str"
+    FAILED_COUNT = 0xFFFFFFFF
+
+    def __init__(self, comm, per, key=None):
+        self.per = max(int(per), 1)
+        self._open(comm, 64 * comm.world, comm.world * self.per * REC, key)
+        self.words = np.ndarray((self.world, 8), dtype=np.int64, buffer=self.shm.buf, offset=64)
+        self.data = np.ndarray((self.world, self.per, REC), dtype=np.uint8, buffer=self.shm.buf,
+                               offset=self.data_off)
+
+    def _drop_views(self):
+        self.words = self.data = None
+
+    def publish(self, lo, hi, block, token):
+        """This rank's records lo .. hi (its shard order), then its progress word."""
+        self.data[self.rank, lo:hi] = block
+        self.words[self.rank, 0] = (int(token) << 32) | int(hi)
+
+    def fail(self, token):
+        self.words[self.rank, 0] = (int(token) << 32) | self.FAILED_COUNT
+
+    def progress(self, token):
+        """Per rank: records published in this call (-1: none yet), FAILED_COUNT: failed."""
+        w = self.words[:, 0].copy()
+        return np.where((w >> 32) == int(token), w & 0xFFFFFFFF, -1)
+
+    def take(self, r, lo, hi):
+        return self.data[r, lo:hi].copy()
 
 
 def run_key():
@@ -611,6 +664,118 @@ def align_sharded_streamed(eng, lengths, pxy, pgap, rank, world, chunks=8, devic
     if node is not None:
         return _exchange_node(shard, chunks, rank, P, default_comm(comm, device, group), node, token)
     return _exchange(shard, chunks, rank, P, default_comm(comm, device, group), final_status=True)
+
+
+def stream_per(lengths, world):
+    """The padded shard size of the per-record exchange (the largest shard)."""
+    return max(shard_sizes(lengths, world) + [1])
+
+
+def align_sharded_records(eng, lengths, pxy, pgap, rank, world, node, token, comm=None, device=None, group=None,
+                          poll_s=20e-6, timeout_s=600.0, on_first=None):
+    """The streamed shard (ONE launch per rank, the fused device finalize) with
+    every record handed to rank 0's chain as soon as it is out: each rank polls
+    its launch (Engine.align_pairs_poll) and publishes the new records into the
+    node segment (NodeStream); rank 0 feeds every record any rank has published
+    to its chain worker, which advances over the canonical prefix as it
+    completes (skel:159).  For uniform lengths the LPT shard is round-robin over
+    canonical ids and every rank aligns its ids in ascending order, so the
+    prefix grows from the first records of all ranks at once.
+    After the launches: ONE all-gather of the padded shards (the collective of
+    record, RCCL on the GPU ranks) that rank 0 checks against the records its
+    chain took, and one status collective.  Failure contract as
+    align_sharded_streamed: a failed rank marks its progress word, joins both
+    collectives with FAILED records, and every rank raises.
+    on_first(): called on rank 0 when its chain has taken the first record.
+    Returns (hash, penalties[P], hashes[P,64]) on rank 0, (None, None, None) elsewhere."""
+    comm = default_comm(comm, device, group)
+    k = len(lengths)
+    P = k * (k - 1) // 2
+    sizes = shard_sizes(lengths, world)
+    per = node.per
+    ids = np.sort(seqalign.shard_pairs(lengths, rank, world))
+    n = len(ids)
+    mine = pack_records([], [], [], per)
+    chain = seqalign.ChainStream(P) if rank == 0 else None
+    taken = np.stack([pack_records([], [], [], per) for _ in range(world)]) if rank == 0 else None
+    seen = [0] * world
+    own_err = None
+    err = None  # a failure rank 0 saw in a progress word
+    pending = False
+    got = 0
+    first = True
+    try:
+        try:
+            eng.align_pairs_begin(ids, pxy, pgap)
+            pending = True
+        except Exception as e:
+            own_err = e
+            node.fail(token)
+        t0 = time.time()
+        while True:
+            moved = False
+            if own_err is None and got < n:
+                try:
+                    u, p_, h_ = eng.align_pairs_poll(got)
+                    if u > got:
+                        blk = pack_records(ids[got:u], p_, h_, u - got)
+                        mine[got:u] = blk
+                        node.publish(got, u, blk, token)
+                        got = u
+                        moved = True
+                except Exception as e:
+                    own_err = e
+                    node.fail(token)
+            own_done = own_err is not None or got >= n
+            if chain is not None and err is None:
+                cnt = node.progress(token)
+                for r in range(world):
+                    c = int(cnt[r])
+                    if c == NodeStream.FAILED_COUNT:
+                        err = RankFailed("rank %d failed while streaming its records" % r)
+                        break
+                    if c > seen[r]:
+                        blk = node.take(r, seen[r], c)
+                        taken[r, seen[r]:c] = blk
+                        cid, cpen, chs = unpack_chunk(blk)
+                        chain.feed(cid, cpen, chs)
+                        if first and on_first is not None:
+                            on_first()
+                        first = False
+                        seen[r] = c
+                        moved = True
+            if own_done and (chain is None or err is not None or all(seen[r] >= sizes[r] for r in range(world))):
+                break
+            if not moved:
+                if time.time() - t0 > timeout_s:
+                    raise RuntimeError("node stream: records not published by every rank in %.0f s" % timeout_s)
+                time.sleep(poll_s)
+        if pending:
+            pending = False
+            try:
+                eng.align_pairs_end()
+            except Exception as e:
+                if own_err is None:
+                    own_err = e
+        g = comm.all_gather(mine if own_err is None else failed_block(per))  # the collective of record
+        err = own_err if own_err is not None else err
+        if any_rank_failed(err is not None, comm) and err is None:
+            err = RankFailed("a peer rank failed")
+        if err is not None:
+            raise RankFailed("rank %d: %s" % (rank, err)) from err
+        if chain is None:
+            return None, None, None
+        if not np.array_equal(np.asarray(g, dtype=np.uint8).reshape(-1, REC), taken.reshape(-1, REC)):
+            raise RuntimeError("rank 0: the all-gathered records differ from the node records the chain took")
+        return chain.finish()
+    finally:
+        if pending:
+            try:
+                eng.align_pairs_end()
+            except Exception:
+                pass
+        if chain is not None:
+            chain.close()
 
 
 def emulate_ranks(make_shard, world, chunks, P):

@@ -114,17 +114,20 @@ def test_bench_nccl_all_gather_at_world_one():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("node", ["1", "0"])
+@pytest.mark.parametrize("node", ["records", "1", "0"])
 def test_two_ranks_streamed_records_big13_published_hash(node):
-    """dist.align_sharded_streamed: one launch per rank (the engine's default
-    task order: largest pairs first, so records arrive in size order, not in
-    canonical order), four pieces each handed to rank 0's chain once all of its
-    records have arrived -- through node shared memory and one all-gather of
-    the whole shards (node=1, dist.NodeRecords, the default on one node), or
-    one all-gather per piece (node=0); the line records when each piece was
-    ready."""
+    """One launch per rank (the engine's default task order: largest pairs
+    first, so records arrive in size order, not in canonical order), the
+    records handed to rank 0's chain -- every record as soon as it is out,
+    through node shared memory (node=records: dist.NodeStream, the default on
+    one node since round 6), or four pieces each once all of its records have
+    arrived, through node shared memory (node=1: dist.NodeRecords) or one
+    all-gather per piece (node=0) -- and one all-gather of the whole shards
+    after the launches; the line records when the chain took its first record,
+    or when each piece was ready."""
     env = _env(NWK_BENCH_BACKEND="gloo", NWK_BENCH_SHARE_GPU="1", NWK_BENCH_WS_GB="110",
-               NWK_BENCH_STREAM="1", NWK_BENCH_CHUNKS="4", NWK_NODE_RECORDS=node)
+               NWK_BENCH_STREAM="1", NWK_BENCH_CHUNKS="4", NWK_NODE_RECORDS="0" if node == "0" else "1",
+               NWK_BENCH_RECORDS="1" if node == "records" else "0")
     r = subprocess.run([sys.executable, "-u", BENCH, "--gpus", "2", "--workload", "big13",
                         "--steps", "1", "--warmup", "0", "--no-cpu-baseline"], stdout=subprocess.PIPE,
                        stderr=subprocess.PIPE, env=env, timeout=110)
@@ -132,6 +135,11 @@ def test_two_ranks_streamed_records_big13_published_hash(node):
     line = json.loads(r.stdout.decode().strip().split("\n")[-1])
     assert line["n_gpus"] == 2 and line["answer_hash_ok"] is True
     assert "streamed" in line["config"]["parallelism"]
+    if node == "records":
+        assert len(line["collective"]["first_record_ms"]) == 1
+        assert line["collective"]["piece_exchange"].startswith("every record through node shared memory")
+        assert line["collective"]["all_gathers_per_step"] == 1
+        return
     ready = line["collective"]["piece_ready_ms"]
     assert len(ready) == 4 and ready == sorted(ready)
     assert line["collective"]["piece_exchange"].startswith("node" if node == "1" else "one all-gather per piece")

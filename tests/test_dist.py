@@ -245,9 +245,10 @@ class _OracleStreamEngine(_OracleEngine):
     fail_end: end() raises after every record has been polled -- the device
     error word that only align_pairs_end reports."""
 
-    def __init__(self, genes, fail_end=False):
+    def __init__(self, genes, fail_end=False, fail_poll=False):
         super().__init__(genes)
         self.fail_end = fail_end
+        self.fail_poll = fail_poll  # poll raises once some records are out (a device error mid-launch)
 
     def align_pairs_begin(self, ids, pxy, pgap):
         super().align_pairs_begin(ids, pxy, pgap)
@@ -255,6 +256,8 @@ class _OracleStreamEngine(_OracleEngine):
         self.ids, self._n = list(ids), 0
 
     def align_pairs_poll(self, start=0):
+        if self.fail_poll and start > 0:
+            raise RuntimeError("injected NWK_EKERNEL while polling")
         self._n = min(len(self.ids), self._n + 3)
         return self._n, self._pen[start:self._n].copy(), self._hs[start:self._n].copy()
 
@@ -279,15 +282,22 @@ def _streamed_worker(rank, world, port, cases, chunks, fail, q, node_records=Fal
         for name, pxy, pgap, genes in cases:
             lens = [len(g) for g in genes]
             node = None
-            if node_records:  # pieces through node shared memory, then ONE all-gather
+            if node_records == "records":  # every record through node shared memory (NodeStream)
+                node = nwdist.NodeStream(nwdist.TorchComm(), nwdist.stream_per(lens, world))
+            elif node_records:  # pieces through node shared memory, then ONE all-gather
                 node = nwdist.NodeRecords(nwdist.TorchComm(), chunks, nwdist.chunk_parts(lens, rank, world, chunks)[1])
             try:
                 for step in range(1, steps + 1):  # (the segment is reused across steps: token = step)
-                    eng = _OracleStreamEngine(genes, fail_end=fail and rank == world - 1)
+                    eng = _OracleStreamEngine(genes, fail_end=fail is True and rank == world - 1,
+                                              fail_poll=fail == "poll" and rank == world - 1)
                     sp, sg = scorings[step - 1] if scorings else (pxy, pgap)
                     try:
-                        h, pen, _ = nwdist.align_sharded_streamed(eng, lens, sp, sg, rank, world, chunks=chunks,
-                                                                  poll_s=0.0, node=node, token=step)
+                        if node_records == "records":
+                            h, pen, _ = nwdist.align_sharded_records(eng, lens, sp, sg, rank, world, node, step,
+                                                                     poll_s=0.0, timeout_s=120.0)
+                        else:
+                            h, pen, _ = nwdist.align_sharded_streamed(eng, lens, sp, sg, rank, world, chunks=chunks,
+                                                                      poll_s=0.0, node=node, token=step)
                         q.put((rank, "%s@%d,%d" % (name, sp, sg) if scorings else name, h,
                                None if pen is None else [int(v) for v in pen]))
                     except nwdist.RankFailed as e:
@@ -299,7 +309,8 @@ def _streamed_worker(rank, world, port, cases, chunks, fail, q, node_records=Fal
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunks,node", [(2, 1, False), (3, 4, False), (2, 1, True), (3, 4, True)])
+@pytest.mark.parametrize("world,chunks,node", [(2, 1, False), (3, 4, False), (2, 1, True), (3, 4, True),
+                                               (2, 1, "records"), (3, 1, "records")])
 def test_gloo_streamed_pieces_match_golden(world, chunks, node):
     """dist.align_sharded_streamed (one launch per rank, records polled as they
     stream; one all-gather per piece, or -- node=True -- the pieces through
@@ -332,8 +343,8 @@ def test_gloo_streamed_pieces_match_golden(world, chunks, node):
             assert h is None
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_node_records_consecutive_calls_different_scorings(world):
+@pytest.mark.parametrize("world,mode", [(2, True), (3, True), (3, "records")])
+def test_gloo_node_records_consecutive_calls_different_scorings(world, mode):
     """consecutive streamed calls with DIFFERENT records on one
     NodeRecords segment.  A peer that has returned publishes its next call's
     pieces into the live segment while rank 0 may still be checking the last
@@ -348,7 +359,7 @@ def test_gloo_node_records_consecutive_calls_different_scorings(world):
     q = ctx.Queue()
     port = _free_port()
     cases = [(c["name"], 0, 0, genes)]
-    procs = [ctx.Process(target=_streamed_worker, args=(r, world, port, cases, 3, False, q, True, len(scorings),
+    procs = [ctx.Process(target=_streamed_worker, args=(r, world, port, cases, 3, False, q, mode, len(scorings),
                                                        scorings)) for r in range(world)]
     for p in procs:
         p.start()
@@ -367,8 +378,9 @@ def test_gloo_node_records_consecutive_calls_different_scorings(world):
             assert h is None
 
 
-@pytest.mark.parametrize("world,node", [(2, False), (3, False), (2, True), (3, True)])
-def test_gloo_streamed_failure_at_end_raises_everywhere(world, node):
+@pytest.mark.parametrize("world,node,fail", [(2, False, True), (3, False, True), (2, True, True), (3, True, True),
+                                             (2, "records", True), (3, "records", True), (3, "records", "poll")])
+def test_gloo_streamed_failure_at_end_raises_everywhere(world, node, fail):
     """The last rank's error surfaces only at align_pairs_end, after all of its
     records were exchanged and chained by rank 0: the final status collective
     makes every rank -- rank 0 included -- raise instead of returning a hash
@@ -378,7 +390,7 @@ def test_gloo_streamed_failure_at_end_raises_everywhere(world, node):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_streamed_worker, args=(r, world, port, cases, 3, True, q, node))
+    procs = [ctx.Process(target=_streamed_worker, args=(r, world, port, cases, 3, fail, q, node))
              for r in range(world)]
     for p in procs:
         p.start()
