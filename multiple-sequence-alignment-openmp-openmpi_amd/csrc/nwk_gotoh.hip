@@ -53,9 +53,14 @@ struct GGeo {
 
 // At least NWK_GOTOH_WPE waves per SIMD: the step is issue-bound and a lone
 // wave issues a VALU op only every ~8 cycles, so occupancy is
-// what fills the SIMD; the probe's step needed 104-117 VGPRs (4 waves fit).
+// what fills the SIMD.  5 (96 VGPRs) since round 6: with the segment loop
+// split in three the fill loops do not spill at 96 (the spills left are per
+// band task), C5 6.58-6.63k -> 6.85k GCUPS; 4 waves take 112 VGPRs.
 #ifndef NWK_GOTOH_WPE
-#define NWK_GOTOH_WPE 4
+#define NWK_GOTOH_WPE 5
+#endif
+#ifndef NWK_GOTOH_STEPSTORE
+#define NWK_GOTOH_STEPSTORE 0
 #endif
 
 // Waits until lanes 0 .. kPl - 1 hold granules tagged `epoch` (v: their last
@@ -321,8 +326,12 @@ __device__ __forceinline__ void trace_gotoh(const FillArgs& a, const PairDesc& p
 
 // ---- fill ----------------------------------------------------------------------
 
+// (scorings with more planes than C5's 8 + 3 keep 4 waves: at 96 VGPRs their step spills)
+template <int GO, int GE>
+constexpr int gotoh_wpe() { return 2 * (GO + GE) + GO <= 11 ? NWK_GOTOH_WPE : 4; }
+
 template <int PXY, int GO, int GE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_WPE))) void nw_align_gotoh(FillArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gotoh_wpe<GO, GE>()))) void nw_align_gotoh(FillArgs a) {
   using C = Cfg<GO, GE, PXY>;
   using G = GGeo<C>;
   constexpr int NV = C::NV, NQ1 = G::NQ1, kPl = G::kPl, kPs = G::kPs;
@@ -397,7 +406,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
     const int capn = a.endv ? pd.n : -100000;
     const int rows_m = pd.m - R0;  // band rows < m
     int cnt = 0;                   // (uniform) planes set over this band's rows < m at column n
-    for (int j = 0; j < nseg; ++j) {
+    // one 32-step segment j; false: the hand-off failed (the task ends)
+    auto segment = [&](int j, auto mask_t, auto end_t) -> bool {
       // --- the row above for lane 0's columns 32 j .. 32 j + 31 -> cons (bit 31 per column)
       {
         unsigned w = 0;  // lane p < kPl: plane p's word (bit r = column 32 j + r)
@@ -410,10 +420,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
             const u64 tw = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
             g = gran_wait<kPl>(gin + (int64_t)j * kPs + lane, a.epoch, g, a.err);
             if (a.stamps) cyc_wait += __builtin_amdgcn_s_memtime() - tw;
-            if (!__all(!gl || (unsigned)(g >> 32) == a.epoch)) {
-              ok = false;
-              break;
-            }
+            if (!__all(!gl || (unsigned)(g >> 32) == a.epoch)) return false;
           }
           w = (unsigned)g;
           if (j < kmax && gl) g = __hip_atomic_load((gu64*)(gin + (int64_t)(j + 1) * kPs + lane), BITS_RLX);
@@ -432,7 +439,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
       }
       const unsigned* yn = ywp + 64 * (j + 1);
       const unsigned nlo0 = yn[0], nlo1 = yn[1];
-      auto seg = [&](auto mask_t, auto end_t) {
+      {
         constexpr bool MASK = decltype(mask_t)::value;
         constexpr bool END = decltype(end_t)::value;
         unsigned dq[4][2];
@@ -501,6 +508,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
             for (int p = 0; p < kPs; p += 4)
               *reinterpret_cast<uint4*>(en_ + p) = make_uint4(ow[p], ow[p + 1], ow[p + 2], ow[p + 3]);
           }
+#if NWK_GOTOH_STEPSTORE
+          // four words per lane and step, one 4-byte store each (the layout of
+          // the 8-byte form below; no staging registers live across steps)
+          {
+            const int rel = (s >> 2) - blo;
+            if ((unsigned)rel < (unsigned)nblk) {
+              unsigned* q = mb + (int64_t)rel * 1024 + (s & 2) * 64 + (s & 1);
+              __builtin_nontemporal_store(D, q);
+              __builtin_nontemporal_store(Fs, q + 256);
+              __builtin_nontemporal_store(Ee, q + 512);
+              __builtin_nontemporal_store(Fe, q + 768);
+            }
+          }
+#else
           // four words per lane and step; every 2 steps one 8-byte store per
           // word, 512 B contiguous across the wave
           dq[0][r & 1] = D;
@@ -517,11 +538,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
                                             reinterpret_cast<u2*>(mb + (int64_t)rel * 1024 + w4 * 256 + (s & 2) * 64));
             }
           }
+#endif
         }
-      };
-      if (j < 65) seg(std::true_type{}, std::true_type{});
-      else if (j >= kmax) seg(std::false_type{}, std::true_type{});
-      else seg(std::false_type{}, std::false_type{});
+      }
       hi0 = lo0;
       hi1 = lo1;
       lo0 = nlo0;
@@ -540,7 +559,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NWK_GOTOH_W
         }
         if (gl) __hip_atomic_store((gu64*)(gout + (int64_t)k * kPs + lane), ((u64)a.epoch << 32) | word, BITS_RLX);
       }
-    }
+      return true;
+    };
+    // three loops, one per form of the step (a branch between the forms inside
+    // one loop made the segment loop irreducible, and the compiler shuffled and
+    // spilled registers at every segment): columns <= 0 masked in the first 65
+    // segments (with the guard's end value for pairs shorter than that), the
+    // plain steps, then the segments that reach column n
+    int j = 0;
+    const int j1 = nseg < 65 ? nseg : 65;
+    for (; j < j1 && ok; ++j) ok = segment(j, std::true_type{}, std::true_type{});
+    for (; j < kmax && ok; ++j) ok = segment(j, std::false_type{}, std::false_type{});
+    for (; j < nseg && ok; ++j) ok = segment(j, std::false_type{}, std::true_type{});
     if (!ok) return;
     if (a.endv) {  // this band's part of H(m, n) (+ the border terms once, band 0)
       const int rows = min(kBR, pd.m - R0);

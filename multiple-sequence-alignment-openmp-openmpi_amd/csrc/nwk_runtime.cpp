@@ -1664,18 +1664,23 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
       for (int q = 0; q < np; ++q) pd[q].prio = (double)pd[q].n + 100.0 * pd[q].nbands >= 0.7 * smax ? 2 : 0;
     }
     // kCol streamed batches (fused finalize: records leave during the launch;
-    // a sharded rank's pairs come in canonical piece order): the first 1/16 of
-    // the pairs dequeued -- a 16-piece rank's first piece -- fill at issue
-    // priority 2 and the next 1/16 at 1, so the first records are out early
-    // and rank 0's chain starts on them while the rest fills.  NWK_PIECE_PRIO=0 disables.
+    // a sharded rank's pairs come in canonical order): the first 1/8 of the
+    // pairs dequeued fill at issue priority 2 and the next 1/8 at 1, so the
+    // lowest canonical ids are out early and rank 0's chain (which consumes
+    // them one record at a time, dist.align_sharded_records) starts on them
+    // while the rest fills.  NWK_PIECE_PRIO=0 disables.
     static const int piece_prio_env = getenv("NWK_PIECE_PRIO") ? atoi(getenv("NWK_PIECE_PRIO")) : 1;
     // (want_fuse: the fused finalize below, asked for or automatic)
     static const int auto_fuse_env = getenv("NWK_AUTO_FUSE") ? atoi(getenv("NWK_AUTO_FUSE")) : 1;
     const bool want_fuse = devhash && bitsy && !sc.affine &&
                            (c->opts.finalize == 3 ||
                             (c->opts.finalize == 0 && auto_fuse_env != 0 && chain && pl.mode == kCol && np >= 8192));
+    // (the first np / div pairs at priority 2, the next np / div at 1; NWK_PIECE_DIV, default 8:
+    // C4 at 8 ranks, chain end 19.85 ms with div 16, 19.05 with 8, 19.63 with 6, profiles/r06/c4_records.txt)
+    static const int piece_div_env = getenv("NWK_PIECE_DIV") ? std::max(2, atoi(getenv("NWK_PIECE_DIV"))) : 8;
     if (pl.mode == kCol && piece_prio_env != 0 && want_fuse && c->opts.finalize == 3 && np >= 32)
-      for (int q = 0; q < np; ++q) pd[q].prio = q < np / 16 ? 2 : q < np / 8 ? std::max(pd[q].prio, 1) : pd[q].prio;
+      for (int q = 0; q < np; ++q)
+        pd[q].prio = q < np / piece_div_env ? 2 : q < 2 * (np / piece_div_env) ? std::max(pd[q].prio, 1) : pd[q].prio;
     if ((rc = c->h_tasks.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
     int2* tk = c->h_tasks.as<int2>();
     // Pair-major (pairs already largest first): a pair's bands are dequeued
