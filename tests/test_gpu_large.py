@@ -112,6 +112,24 @@ def test_c5_affine_scores_vs_oracle(engine):
     assert [int(v) for v in pl] == [s["linear_penalty"] for s in g["scores"]]
 
 
+@pytest.mark.skipif(not os.path.exists(os.path.join(LARGE, "c5_pen.json")), reason="c5_pen.json not generated")
+def test_c5_affine_all_penalties_vs_oracle(engine):
+    """C5 at full size with its affine scoring (go=3, ge=1: the bench's config),
+    every one of the 496 penalties against the oracle's O(n)-memory Gotoh scorer
+    (tests/golden/large/c5_pen.json; the affine variant has no reference, SURVEY
+    §8 a9), through getMinimumPenalties on the engine: nw_align_gotoh, W = 8192
+    windowed storage, the fill-vs-walk guard on every pair."""
+    g = _fixture("c5_pen")
+    _, k, L, pxy, pgap, (go, ge) = workloads.SYNTH["c5"]
+    assert (g["k"], g["L"], g["pxy"], g["go"], g["ge"]) == (k, L, pxy, go, ge)
+    genes = workloads.synth(k, L)
+    engine.set_sequences(genes)
+    _, pen, _ = engine.align_all(pxy, None, affine=(go, ge))
+    st = engine.stats()
+    assert [int(v) for v in pen] == g["penalties"]
+    assert st["mode"] == 11 and st.get("guard_reruns", 0) == 0
+
+
 def test_affine_window_choice_at_a_large_budget():
     """nw_align_pka's storage window at a budget above 2^33 B (the runtime used
     to multiply the budget by 2^30 and overflow there): k=8 x 30k affine needs
