@@ -516,6 +516,40 @@ def test_node_records_stale_segment_is_replaced():
         stale.close()
 
 
+def test_node_stream_stale_segment_progress_and_failure():
+    """NodeStream: rank 0 replaces a stale segment of the same name; progress
+    words carry this call's token (an earlier call's count reads as -1), a
+    publish moves the count after the records, and a failed rank's word reads
+    FAILED_COUNT (world 1)."""
+    import sys
+    from multiprocessing import shared_memory
+
+    sys.path.insert(0, PKG)
+    import dist as nwdist
+
+    class One:
+        world, rank = 1, 0
+
+        def max(self, x):
+            return x
+
+    key = "s%d" % os.getpid()
+    stale = shared_memory.SharedMemory(name="nwk_str_" + key, create=True, size=4096)
+    stale.buf[:8] = b"\xff" * 8
+    try:
+        ns = nwdist.NodeStream(One(), 4, key=key)
+        assert list(ns.progress(1)) == [-1]  # cleared words: no record of this call yet
+        blk = nwdist.pack_records([5, 6], [10, 11], np.full((2, 64), 9, dtype=np.uint8), 2)
+        ns.publish(0, 2, blk, 3)
+        assert list(ns.progress(3)) == [2] and list(ns.progress(4)) == [-1]
+        assert (ns.take(0, 0, 2) == blk).all()
+        ns.fail(4)
+        assert list(ns.progress(4)) == [nwdist.NodeStream.FAILED_COUNT]
+        ns.close()
+    finally:
+        stale.close()
+
+
 def test_node_records_fast_peer_flag_survives():
     """NodeRecords: a peer may publish as soon as rank 0's nonce collective
     returns to it, before rank 0's own constructor has finished -- its flag
