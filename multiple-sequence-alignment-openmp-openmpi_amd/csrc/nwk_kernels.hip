@@ -1801,22 +1801,30 @@ __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairD
       return true;
     };
     if (diag_try && diag_run()) {
+    } else if constexpr (LIN) {
+      // Every lane packs its cell's move byte, the lane of the cell the move
+      // leads to, whether that cell is still inside the block, and its block
+      // coordinates; the scalar walk is then one v_readlane + one s_bfe per move
+      // (round 6: ~8 instructions a move, was ~30 -- decode, bounds, index).
+      const unsigned src = code & 3u;
+      const int nli = li + (int)((3u >> src) & 1u), nlj = lj + (int)((5u >> src) & 1u);
+      // (a code the fill never writes, 3, ends the walk: its cell is an exit with bit 17 set)
+      const unsigned pk = ((0x6c7544u >> (8 * src)) & 0xffu) | ((unsigned)(nli * 8 + nlj) << 8) |
+                          (nli < li_lim && nlj < lj_lim && src != 3u ? 1u << 16 : 0u) | (src == 3u ? 1u << 17 : 0u) |
+                          ((unsigned)nli << 20) | ((unsigned)nlj << 24);
+      int cur = 0;
+      unsigned p;
+      do {  // one exit: the move leaves the block (or reaches row / column 0)
+        p = (unsigned)__builtin_amdgcn_readlane((int)pk, cur);
+        asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(p & 0xffu) : "memory");  // 'D', 'u', 'l'
+        ++Lc;
+        cur = (int)((p >> 8) & 63u);
+      } while (p & (1u << 16));
+      bad = bad || (p & (1u << 17));  // (the walk fails: err 16 below)
+      di = (int)((p >> 20) & 15u);
+      dj = (int)((p >> 24) & 15u);
     } else for (;;) {
       const unsigned c = __builtin_amdgcn_readlane(code, di * 8 + dj);
-      if constexpr (LIN) {
-        const unsigned src = c & 3u;
-        if (src == 3u) {
-          bad = true;  // not a code the fill writes
-          break;
-        }
-        const unsigned op = (0x6c7544u >> (8 * src)) & 0xffu;  // 'D', 'u', 'l'
-        di += (3u >> src) & 1u;
-        dj += (5u >> src) & 1u;
-        asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(op) : "memory");
-        ++Lc;
-        if (di >= li_lim || dj >= lj_lim) break;
-        continue;
-      }
       unsigned op;
       op = 0;
       if (st == 0) {

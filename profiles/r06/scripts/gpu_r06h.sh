@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
-# Round-6 session h: nw_profile with the two-rows-per-min3 chain (MSA tests
-# against the oracle, msa_bench).
+# Round-6 session h: nw_profile changes (MSA tests
+# against the oracle, msa_bench): the min3 chain (not kept), then the packed-lane walk.
 set -u
 cd "$(dirname "$0")/../../.."
 O=gpurun_out/r06h; mkdir -p $O
