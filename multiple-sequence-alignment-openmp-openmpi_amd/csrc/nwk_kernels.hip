@@ -1717,16 +1717,21 @@ __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairD
   const int ncols = 64 * pd.sblocks / SPD;
   const unsigned* mb = a.mat + pd.mat_off;
   const int lane_off = (lane >> 4) * kWave + (lane & 15);
-  auto issue = [&](int b, int q, int t0) {
+  unsigned* curt = &L.tile[0][0];  // the tile the walk reads
+  auto issue = [&](int b, int q, int t0, unsigned* dst) {
     const unsigned* src = mb + (int64_t)b * bdw + t0 + lane_off;
 #pragma unroll
     for (int k = 0; k < C::TILE / 64; ++k) {
       int c = C::TC * q - C::OV + (k >> 1);
       c = c < 0 ? 0 : (c >= ncols ? ncols - 1 : c);
       __builtin_amdgcn_global_load_lds((gbl_void*)(src + (int64_t)c * (kRows * kWave) + (k & 1) * 4 * kWave),
-                                       (lds_void*)&L.tile[0][64 * k], 4, 0, 0);
+                                       (lds_void*)(dst + 64 * k), 4, 0, 0);
     }
   };
+  // (nwk_msa verbose >= 2) walk cycles: tile switches, code reads, blocks, switches
+  const bool wst = LIN && a.stamps != nullptr;
+  u64 c_sw = 0, c_rd = 0, n_blk = 0, n_sw = 0;
+  const u64 c_w0 = wst ? __builtin_amdgcn_s_memtime() : 0;
   auto drain = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
   uint8_t* ops = a.ops + pd.ops_off;
   int i = pd.m, j = pd.n, Lc = 0, flushed = 0, tb = -1, tq = 0, tt0 = 0;
@@ -1754,16 +1759,21 @@ __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairD
       const int tl = t > 0 ? t - 1 : 0;
       const int s = j - 1 + t;
       if (b != tb || s < C::TS * tq || tl < tt0 || t >= tt0 + C::TL) {
+        const u64 cs0 = wst ? __builtin_amdgcn_s_memtime() : 0;
+        ++n_sw;
         const int q = s / C::TS;
         drain();
         flush(Lc & ~3);
         const int nt0 = max(0, t - (C::TL - 3));
-        issue(b, q, nt0);
+        issue(b, q, nt0, curt);
         drain();
         tb = b; tq = q; tt0 = nt0;
+        if (wst) c_sw += __builtin_amdgcn_s_memtime() - cs0;
       }
     }
     // this lane's cell (ci, cj) = (i - li, j - lj)
+    ++n_blk;
+    const u64 cr0 = wst ? __builtin_amdgcn_s_memtime() : 0;
     const int ci = i - li, cj = j - lj;
     unsigned code = 0;
     if (ci >= 1 && cj >= 1) {
@@ -1773,12 +1783,16 @@ __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairD
       const int cbase = C::TC * tq - C::OV;
       unsigned v;
       if (ww >= 0 && tt >= tt0 && tt < tt0 + C::TL && ss >= slo && ss < shi) {
-        const unsigned ad = lds_addr(&L.tile[0][0]) + 4u * (unsigned)(((ss / SPD - cbase) * kRows + rr) * C::TL + (tt - tt0));
+        const unsigned ad = lds_addr(curt) + 4u * (unsigned)(((ss / SPD - cbase) * kRows + rr) * C::TL + (tt - tt0));
         asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ad) : "memory");
         code = (v >> (4 * (ss & (SPD - 1)))) & 15u;
       } else {
         code = getG_global<4, 0>(a.mat, pd, bdw, ci, cj);
       }
+    }
+    if (wst) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      c_rd += __builtin_amdgcn_s_memtime() - cr0;
     }
     if (prog && lane == 0) __hip_atomic_store((gu32*)prog, 0x51000000u | (code & 0xff) << 8 | (nit & 0xff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // scalar walk through the block
@@ -1872,6 +1886,14 @@ __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairD
   if (lane == 0) {
     a.oplen[pd.slot] = Lc;
     a.endij[pd.slot] = make_int2(i, j);
+  }
+  if (wst && lane == 0) {
+    u64* x = a.stamps + 8 * pd.slot;
+    x[2] = __builtin_amdgcn_s_memtime() - c_w0;
+    x[3] = c_sw;
+    x[4] = c_rd;
+    x[5] = (n_blk << 32) | n_sw;
+    x[6] = (unsigned)Lc;
   }
 }
 
@@ -2764,10 +2786,11 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       PROG(0x40000000u);
-      // nwk_msa verbose >= 2: {walk start, walk end} per merge (s_memrealtime, 100 MHz)
-      if (a.stamps && lane == 0) a.stamps[2 * pd.slot] = __builtin_amdgcn_s_memrealtime();
+      // nwk_msa verbose >= 2: per merge 8 u64, {walk start, walk end} (s_memrealtime, 100 MHz), then
+      // the walk's cycle counters (trace_pair_affine<true>)
+      if (a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
       trace_pair_affine<true>(a, pd, tbl[wid], lane, prog);
-      if (a.stamps && lane == 0) a.stamps[2 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
+      if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
       PROG(0x60000000u);
     }
   }

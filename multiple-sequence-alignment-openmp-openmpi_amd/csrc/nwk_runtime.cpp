@@ -3238,8 +3238,8 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       fflush(stderr);
     }
     if (c->opts.verbose >= 2) {
-      if ((rc = c->d_stamps.ensure(16 * (size_t)np)) != NWK_OK) return rc;
-      HIP_TRY(hipMemsetAsync(c->d_stamps.p, 0, 16 * (size_t)np, c->stream));
+      if ((rc = c->d_stamps.ensure(64 * (size_t)np)) != NWK_OK) return rc;
+      HIP_TRY(hipMemsetAsync(c->d_stamps.p, 0, 64 * (size_t)np, c->stream));
       fa.stamps = c->d_stamps.as<unsigned long long>();
     }
     t_prep = now_ms();
@@ -3266,17 +3266,24 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
     ++st.fill_launches;
     ++st.batches;
     if (c->opts.verbose >= 2) {
-      std::vector<unsigned long long> sw((size_t)2 * np);
-      HIP_TRY(hipMemcpy(sw.data(), fa.stamps, 16 * (size_t)np, hipMemcpyDeviceToHost));
+      // per merge (8 u64): walk start / end (s_memrealtime, 100 MHz), then walk cycles
+      // (s_memtime), of which tile switches and code reads, blocks << 32 | switches, moves
+      std::vector<unsigned long long> sw((size_t)8 * np);
+      HIP_TRY(hipMemcpy(sw.data(), fa.stamps, 64 * (size_t)np, hipMemcpyDeviceToHost));
       double wmax = 0, wsum = 0;
+      int qm = 0;
       for (int q = 0; q < np; ++q) {
-        const double w = sw[2 * q + 1] > sw[2 * q] ? (sw[2 * q + 1] - sw[2 * q]) * 1e-5 : 0.0;  // 100 MHz ticks -> ms
-        wmax = std::max(wmax, w);
+        const double w = sw[8 * q + 1] > sw[8 * q] ? (sw[8 * q + 1] - sw[8 * q]) * 1e-5 : 0.0;  // 100 MHz ticks -> ms
+        if (w > wmax) wmax = w, qm = q;
         wsum += w;
       }
-      fprintf(stderr, "nwk_msa level %d: %d merges, %lld band tasks, %.3f ms (walks: longest %.3f ms, sum %.3f ms); host: "
-              "previous merges + profiles %.3f ms, uploads %.3f ms, launch to results %.3f ms\n", rd, np,
-              (long long)ntasks, (double)lvl_ms, wmax, wsum, t_build - t_lvl, t_prep - t_build, t_wait - t_prep);
+      const unsigned long long* x = &sw[8 * (size_t)qm];
+      fprintf(stderr, "nwk_msa level %d: %d merges, %lld band tasks, %.3f ms (walks: longest %.3f ms, sum %.3f ms; "
+              "longest: %llu cycles, tile switches %.1f%%, code reads %.1f%%, %llu blocks, %llu switches, %llu "
+              "moves); host: previous merges + profiles %.3f ms, uploads %.3f ms, launch to results "
+              "%.3f ms\n", rd, np, (long long)ntasks, (double)lvl_ms, wmax, wsum, x[2], x[2] ? 100.0 * x[3] / x[2] : 0.0,
+              x[2] ? 100.0 * x[4] / x[2] : 0.0, x[5] >> 32, x[5] & 0xffffffffull, x[6] & 0xffffffffull,
+              t_build - t_lvl, t_prep - t_build, t_wait - t_prep);
     }
     // ---- merged profiles and merge costs (forward moves: prefix run, then the reversed trace)
     for (int q = 0; q < np; ++q) {

@@ -5,5 +5,6 @@ cd "$(dirname "$0")/../../.."
 O=gpurun_out/r06j; mkdir -p $O
 export TMPDIR=/tmp
 step() { local name=$1 lim=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 $lim "$@" > $O/$name.out 2>&1; local rc=$?; tail -4 $O/$name.out | cut -c1-300; echo "$name rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
-step levels_k16 200 python -u tools/msa_bench.py --reps 3 --sets 16:10000 --levels
-step k16_again 200 python -u tools/msa_bench.py --reps 3 --sets 16:10000,16:10000
+
+step levels_k64 200 python -u tools/msa_bench.py --reps 1 --sets 64:5000 --levels
+
