@@ -41,8 +41,25 @@ import seqalign
 REC = 72
 
 
+_SHARDS = {}
+
+
+def all_shards(lengths, world):
+    """Every rank's LPT shard (seqalign.shard_pairs, ascending ids), computed once
+    per (lengths, world): the streamed paths need all of them every step, and
+    C4's eight shards cost ~20 ms of host time (inside the timed step) uncached."""
+    key = (world, np.asarray(lengths, dtype=np.int64).tobytes())
+    got = _SHARDS.get(key)
+    if got is None:
+        got = [np.sort(seqalign.shard_pairs(lengths, r, world)) for r in range(world)]
+        if len(_SHARDS) > 8:
+            _SHARDS.clear()
+        _SHARDS[key] = got
+    return got
+
+
 def shard_sizes(lengths, world):
-    return [len(seqalign.shard_pairs(lengths, r, world)) for r in range(world)]
+    return [len(x) for x in all_shards(lengths, world)]
 
 
 def pack_records(ids, penalties, hashes, per):
@@ -236,7 +253,7 @@ def chunk_parts(lengths, rank, world, chunks):
     P = k * (k - 1) // 2
     bounds = [P * c // chunks for c in range(chunks + 1)]
     cut = lambda ids, c: ids[(ids >= bounds[c]) & (ids < bounds[c + 1])]
-    shards = [seqalign.shard_pairs(lengths, r, world) for r in range(world)]
+    shards = all_shards(lengths, world)
     per = [max([len(cut(sh, c)) for sh in shards] + [1]) for c in range(chunks)]
     return [cut(shards[rank], c) for c in range(chunks)], per
 
@@ -693,7 +710,7 @@ def align_sharded_records(eng, lengths, pxy, pgap, rank, world, node, token, com
     P = k * (k - 1) // 2
     sizes = shard_sizes(lengths, world)
     per = node.per
-    ids = np.sort(seqalign.shard_pairs(lengths, rank, world))
+    ids = all_shards(lengths, world)[rank]
     n = len(ids)
     mine = pack_records([], [], [], per)
     chain = seqalign.ChainStream(P) if rank == 0 else None
