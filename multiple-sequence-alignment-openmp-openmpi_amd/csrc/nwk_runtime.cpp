@@ -1677,10 +1677,17 @@ int align_work(nwk_ctx* c, std::vector<PairWork>& work, const Scoring& sc, int32
                             (c->opts.finalize == 0 && auto_fuse_env != 0 && chain && pl.mode == kCol && np >= 8192));
     // (the first np / div pairs at priority 2, the next np / div at 1; NWK_PIECE_DIV, default 8:
     // C4 at 8 ranks, chain end 19.85 ms with div 16, 19.05 with 8, 19.63 with 6, profiles/r06/c4_records.txt)
+    // NWK_PIECE_TOP (experiment, default 2): the first tier's priority; each next
+    // np / div pairs one lower, down to 1 (3: the first tier issues level with the walks)
     static const int piece_div_env = getenv("NWK_PIECE_DIV") ? std::max(2, atoi(getenv("NWK_PIECE_DIV"))) : 8;
-    if (pl.mode == kCol && piece_prio_env != 0 && want_fuse && c->opts.finalize == 3 && np >= 32)
-      for (int q = 0; q < np; ++q)
-        pd[q].prio = q < np / piece_div_env ? 2 : q < 2 * (np / piece_div_env) ? std::max(pd[q].prio, 1) : pd[q].prio;
+    static const int piece_top_env = getenv("NWK_PIECE_TOP") ? std::min(3, std::max(1, atoi(getenv("NWK_PIECE_TOP")))) : 2;
+    if (pl.mode == kCol && piece_prio_env != 0 && want_fuse && c->opts.finalize == 3 && np >= 32) {
+      const int tier = std::max(1, np / piece_div_env);
+      for (int q = 0; q < np; ++q) {
+        const int pr = piece_top_env - q / tier;
+        if (pr >= 1) pd[q].prio = std::max(pd[q].prio, pr);
+      }
+    }
     if ((rc = c->h_tasks.ensure(sizeof(int2) * ntasks)) != NWK_OK) return rc;
     int2* tk = c->h_tasks.as<int2>();
     // Pair-major (pairs already largest first): a pair's bands are dequeued
