@@ -2718,7 +2718,12 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
             }
             const unsigned d = (r ? h[r - 1] : dg0) + 4u * sub;  // diag: row above, previous step
             const unsigned key = min(min(d, h[r] + lk), hp + gxk[r]);
-            acc[r] = __builtin_amdgcn_alignbit(key | 12u, acc[r], 4);
+            // (the code nibble is key's low 4 bits with both "opened" bits set: the
+            // | 12 of all eight nibbles is one v_or at the store; the empty asm keeps
+            // the shift in this step -- sunk to the store, it held 56 keys in
+            // registers, with a v_mov each)
+            acc[r] = __builtin_amdgcn_alignbit(key, acc[r], 4);
+            asm volatile("" : "+v"(acc[r]));
             const unsigned nv = key & ~3u;
             nh[r] = MASK ? (valid ? nv : h[r]) : nv;
             hp = nh[r];
@@ -2731,7 +2736,7 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
           }
           if (k == 7) {
 #pragma unroll
-            for (int r = 0; r < kRows; ++r) __builtin_nontemporal_store(acc[r], mptr + r * kWave);
+            for (int r = 0; r < kRows; ++r) __builtin_nontemporal_store(acc[r] | 0xccccccccu, mptr + r * kWave);
           }
           __builtin_amdgcn_sched_barrier(0);
         }

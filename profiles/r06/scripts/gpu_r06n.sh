@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round-6 session n: nw_profile's walk on the scalar unit from two ballots
+# Round-6 session n: nw_profile A/B runs (tree vs abv6 variant): first the scalar walk, then the per-step code accumulation.
 # (NWK_PROF_SWALK=1, the tree) vs the packed-lane v_readlane walk (abv6/pk).
 set -u
 cd "$(dirname "$0")/../../.."
@@ -7,7 +7,7 @@ O=gpurun_out/r06n; mkdir -p $O
 export TMPDIR=/tmp
 step() { local name=$1 lim=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 $lim "$@" > $O/$name.out 2>&1; local rc=$?; tail -2 $O/$name.out | cut -c1-300; echo "$name rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
 step msa_tests 300 python -u -m pytest tests/test_gpu.py tests/test_gpu_guard.py -x -q --timeout 150 --timeout-method thread -p no:cacheprovider -k "msa or profile"
-step levels_sw 200 python -u tools/msa_bench.py --reps 1 --sets 64:5000 --levels
-NWK_LIB=abv6/pk/libnwk.so step levels_pk 200 python -u tools/msa_bench.py --reps 1 --sets 64:5000 --levels
-step bench_sw 300 python -u tools/msa_bench.py --reps 3 --sets 64:5000,8:50000,256:2000
-NWK_LIB=abv6/pk/libnwk.so step bench_pk 300 python -u tools/msa_bench.py --reps 3 --sets 64:5000,8:50000,256:2000
+step levels_new 200 python -u tools/msa_bench.py --reps 1 --sets 64:5000 --levels
+NWK_LIB=abv6/base/libnwk.so step levels_base 200 python -u tools/msa_bench.py --reps 1 --sets 64:5000 --levels
+step bench_new 300 python -u tools/msa_bench.py --reps 3 --sets 64:5000,8:50000,256:2000
+NWK_LIB=abv6/base/libnwk.so step bench_base 300 python -u tools/msa_bench.py --reps 3 --sets 64:5000,8:50000,256:2000
