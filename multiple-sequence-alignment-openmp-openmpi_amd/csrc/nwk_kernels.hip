@@ -150,6 +150,9 @@ __device__ __forceinline__ unsigned opaque_zero32() {
 // kernel's HBM writes, tools/pka_write_probe.py), so a wait backs off: the
 // sleep doubles from ~0.1 us to ~1.6 us (s_sleep n = 64 n cycles) -- a
 // 64-column chunk takes a band ~15 us, so the wait still ends within ~10%.
+#ifndef NWK_WALK_JUMP  // trace_pair_affine<LIN>: a block's path by pointer doubling
+#define NWK_WALK_JUMP 2
+#endif
 #ifndef NWK_POLL_SLEEP_MAX
 #define NWK_POLL_SLEEP_MAX 32
 #endif
@@ -1826,14 +1829,58 @@ __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairD
       const unsigned pk = ((0x6c7544u >> (8 * src)) & 0xffu) | ((unsigned)(nli * 8 + nlj) << 8) |
                           (nli < li_lim && nlj < lj_lim && src != 3u ? 1u << 16 : 0u) | (src == 3u ? 1u << 17 : 0u) |
                           ((unsigned)nli << 20) | ((unsigned)nlj << 24);
-      int cur = 0;
       unsigned p;
+#if NWK_WALK_JUMP
+      // Pointer doubling instead of the serial chain: nx = the next lane on the path
+      // (a lane whose move leaves the block points at itself), J2/J4/J8 = nx^2/^4/^8,
+      // then lane t finds the path's t-th cell X_t = nx^t(0) (t <= 15: a block path
+      // has at most 15 moves) and its packed move. The moves are lanes 0..T, T = the
+      // count of in-block X_t; they go out as one lane-masked LDS write.
+      {
+        const unsigned nx = (pk & (1u << 16)) ? (pk >> 8) & 63u : (unsigned)lane;
+#if NWK_WALK_JUMP == 2
+        // (five LDS round trips: the path prefix X_0..X_{2k-1} grows by a DPP row
+        // shift of X_0..X_{k-1} and one bpermute of J_k, issued with J_2k's)
+        unsigned x = lane == 1 ? (unsigned)__builtin_amdgcn_readlane((int)nx, 0) : 0u;
+        const unsigned j2 = (unsigned)__builtin_amdgcn_ds_bpermute((int)(nx << 2), (int)nx);
+        unsigned y = (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x112 /*row_shr:2*/, 0xf, 0xf, false);
+        const unsigned x2 = (unsigned)__builtin_amdgcn_ds_bpermute((int)(y << 2), (int)j2);
+        const unsigned j4 = (unsigned)__builtin_amdgcn_ds_bpermute((int)(j2 << 2), (int)j2);
+        x = (lane & 14) == 2 ? x2 : x;
+        y = (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x114 /*row_shr:4*/, 0xf, 0xf, false);
+        const unsigned x4 = (unsigned)__builtin_amdgcn_ds_bpermute((int)(y << 2), (int)j4);
+        const unsigned j8 = (unsigned)__builtin_amdgcn_ds_bpermute((int)(j4 << 2), (int)j4);
+        x = (lane & 12) == 4 ? x4 : x;
+        y = (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x118 /*row_shr:8*/, 0xf, 0xf, false);
+        const unsigned x8 = (unsigned)__builtin_amdgcn_ds_bpermute((int)(y << 2), (int)j8);
+        x = (lane & 8) ? x8 : x;
+#else
+        const unsigned j2 = (unsigned)__builtin_amdgcn_ds_bpermute((int)(nx << 2), (int)nx);
+        const unsigned j4 = (unsigned)__builtin_amdgcn_ds_bpermute((int)(j2 << 2), (int)j2);
+        const unsigned j8 = (unsigned)__builtin_amdgcn_ds_bpermute((int)(j4 << 2), (int)j4);
+        unsigned x = (lane & 1) ? (unsigned)__builtin_amdgcn_readlane((int)nx, 0) : 0u;
+        const unsigned x2 = (unsigned)__builtin_amdgcn_ds_bpermute((int)(x << 2), (int)j2);
+        x = (lane & 2) ? x2 : x;
+        const unsigned x4 = (unsigned)__builtin_amdgcn_ds_bpermute((int)(x << 2), (int)j4);
+        x = (lane & 4) ? x4 : x;
+        const unsigned x8 = (unsigned)__builtin_amdgcn_ds_bpermute((int)(x << 2), (int)j8);
+        x = (lane & 8) ? x8 : x;
+#endif
+        const unsigned px = (unsigned)__builtin_amdgcn_ds_bpermute((int)(x << 2), (int)pk);
+        const int T = __popcll(__ballot(lane < 16 && (px & (1u << 16))));
+        if (lane <= T) asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)((Lc + lane) & 255)), "v"(px & 0xffu) : "memory");  // 'D', 'u', 'l'
+        Lc += T + 1;
+        p = (unsigned)__builtin_amdgcn_readlane((int)px, T);
+      }
+#else
+      int cur = 0;
       do {  // one exit: the move leaves the block (or reaches row / column 0)
         p = (unsigned)__builtin_amdgcn_readlane((int)pk, cur);
         asm volatile("ds_write_b8 %0, %1" ::"v"(ob + (unsigned)(Lc & 255)), "v"(p & 0xffu) : "memory");  // 'D', 'u', 'l'
         ++Lc;
         cur = (int)((p >> 8) & 63u);
       } while (p & (1u << 16));
+#endif
       bad = bad || (p & (1u << 17));  // (the walk fails: err 16 below)
       di = (int)((p >> 20) & 15u);
       dj = (int)((p >> 24) & 15u);

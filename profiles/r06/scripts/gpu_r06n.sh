@@ -1,6 +1,5 @@
 #!/usr/bin/env bash
-# Round-6 session n: nw_profile A/B runs (tree vs abv6 variant): first the scalar walk, then the per-step code accumulation.
-# (NWK_PROF_SWALK=1, the tree) vs the packed-lane v_readlane walk (abv6/pk).
+# Round-6 session n: nw_profile A/B runs (tree vs abv6/base variant): pointer-doubling block walk, 5 LDS round trips (NWK_WALK_JUMP 2) vs 7 (1).
 set -u
 cd "$(dirname "$0")/../../.."
 O=gpurun_out/r06n; mkdir -p $O
