@@ -28,6 +28,7 @@
 // broadcast ds_read_b128.  Bands are dequeued from one atomic head in
 // dependency order, so a wave only ever waits on a band dequeued earlier.
 #include "nwk_internal.h"
+#include "nwk_prof.h"
 
 namespace nwk {
 
@@ -1712,22 +1713,27 @@ __device__ __forceinline__ void wait_vm_keep4(unsigned&, unsigned&, u64&, u64&) 
 // charges go + ge there, ge for the others).
 // LIN: every code is a fresh move (nw_profile's linear gaps set both "opened"
 // bits), so the walk needs no gap state: a cell's two low bits are its move.
-template <bool LIN = false>
+template <bool LIN = false, int R = kRows>
 __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairDesc& pd, TbLds<4>& L, int lane, unsigned* prog) {
   using C = TbConf<4>;
   constexpr int SPD = C::SPC;
-  const int64_t bdw = band_dwords(4, pd.sblocks);
+  // R rows per lane (nw_profile: kProfRows): a band is 64 R rows; a tile keeps
+  // the same dwords as R = 8's 16 lanes x 8 rows, so it holds TLR = 128 / R lanes
+  constexpr int BR = kWave * R, LR = R == 8 ? 3 : 2, TLR = C::TL * kRows / R;
+  constexpr int DPC = R * TLR / 64, RPD = 64 / TLR;  // DMAs per column unit, rows per DMA
+  static_assert(R == 8 || R == 4, "trace_pair_affine: 4 or 8 rows per lane");
+  const int64_t bdw = (int64_t)pd.sblocks * (64 / SPD) * R * kWave;
   const int ncols = 64 * pd.sblocks / SPD;
   const unsigned* mb = a.mat + pd.mat_off;
-  const int lane_off = (lane >> 4) * kWave + (lane & 15);
+  const int lane_off = (lane / TLR) * kWave + (lane % TLR);
   unsigned* curt = &L.tile[0][0];  // the tile the walk reads
   auto issue = [&](int b, int q, int t0, unsigned* dst) {
     const unsigned* src = mb + (int64_t)b * bdw + t0 + lane_off;
 #pragma unroll
     for (int k = 0; k < C::TILE / 64; ++k) {
-      int c = C::TC * q - C::OV + (k >> 1);
+      int c = C::TC * q - C::OV + k / DPC;
       c = c < 0 ? 0 : (c >= ncols ? ncols - 1 : c);
-      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (int64_t)c * (kRows * kWave) + (k & 1) * 4 * kWave),
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + (int64_t)c * (R * kWave) + (k % DPC) * RPD * kWave),
                                        (lds_void*)(dst + 64 * k), 4, 0, 0);
     }
   };
@@ -1755,19 +1761,19 @@ __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairD
   while (i > 0 && j > 0) {
     ++nit;
     if (prog && lane == 0) __hip_atomic_store((gu32*)prog, 0x50000000u | ((nit & 0xff) << 20) | ((unsigned)(i & 0x3ff) << 10) | (unsigned)(j & 0x3ff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const int w = (i - 1) & (kBandRows - 1);
-    const int t = w >> 3;
-    const int b = (i - 1) / kBandRows;
+    const int w = (i - 1) & (BR - 1);
+    const int t = w >> LR;
+    const int b = (i - 1) / BR;
     {
-      const int tl = t > 0 ? t - 1 : 0;
+      const int tl = max(t - (R + 6) / R, 0);  // the lane of the block's top row
       const int s = j - 1 + t;
-      if (b != tb || s < C::TS * tq || tl < tt0 || t >= tt0 + C::TL) {
+      if (b != tb || s < C::TS * tq || tl < tt0 || t >= tt0 + TLR) {
         const u64 cs0 = wst ? __builtin_amdgcn_s_memtime() : 0;
         ++n_sw;
         const int q = s / C::TS;
         drain();
         flush(Lc & ~3);
-        const int nt0 = max(0, t - (C::TL - 3));
+        const int nt0 = max(0, t - (TLR - 3));
         issue(b, q, nt0, curt);
         drain();
         tb = b; tq = q; tt0 = nt0;
@@ -1780,17 +1786,23 @@ __device__ __forceinline__ void trace_pair_affine(const FillArgs& a, const PairD
     const int ci = i - li, cj = j - lj;
     unsigned code = 0;
     if (ci >= 1 && cj >= 1) {
-      const int ww = ci - 1 - tb * kBandRows;
-      const int tt = ww >> 3, rr = ww & 7, ss = cj - 1 + tt;
+      const int ww = ci - 1 - tb * BR;
+      const int tt = ww >> LR, rr = ww & (R - 1), ss = cj - 1 + tt;
       const int slo = C::TS * tq - C::OV * SPD, shi = C::TS * tq + C::TS;
       const int cbase = C::TC * tq - C::OV;
       unsigned v;
-      if (ww >= 0 && tt >= tt0 && tt < tt0 + C::TL && ss >= slo && ss < shi) {
-        const unsigned ad = lds_addr(curt) + 4u * (unsigned)(((ss / SPD - cbase) * kRows + rr) * C::TL + (tt - tt0));
+      if (ww >= 0 && tt >= tt0 && tt < tt0 + TLR && ss >= slo && ss < shi) {
+        const unsigned ad = lds_addr(curt) + 4u * (unsigned)(((ss / SPD - cbase) * R + rr) * TLR + (tt - tt0));
         asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ad) : "memory");
         code = (v >> (4 * (ss & (SPD - 1)))) & 15u;
       } else {
-        code = getG_global<4, 0>(a.mat, pd, bdw, ci, cj);
+        if constexpr (R == kRows) {
+          code = getG_global<4, 0>(a.mat, pd, bdw, ci, cj);
+        } else {  // (same layout, R rows per lane)
+          const int w1 = ci - 1, b1 = w1 / BR, t1 = (w1 - b1 * BR) >> LR, r1 = (w1 - b1 * BR) & (R - 1);
+          const int s1 = cj - 1 + t1;
+          code = (mb[(int64_t)b1 * bdw + ((int64_t)(s1 / SPD) * R + r1) * kWave + t1] >> (4 * (s1 & (SPD - 1)))) & 15u;
+        }
       }
     }
     if (wst) {
@@ -2652,7 +2664,7 @@ __device__ __forceinline__ unsigned prof_sub(const unsigned (&rp)[N], const int4
   }
 }
 
-template <int DOT>
+template <int DOT, int R = kProfRows>
 __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
   constexpr int W = 4, SPD = 8;
   constexpr int NP = DOT >= 4 ? 2 : DOT == 2 ? 3 : 6;  // packed ints per profile entry
@@ -2674,10 +2686,10 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
     const int2 task = a.tasks[tk];
     const PairDesc pd = a.pairs[task.x];
     const int band = task.y;
-    const int row0 = band * kBandRows + lane * kRows;  // 0-based first DP row of this lane
-    unsigned rp[kRows][NP], gxk[kRows], h[kRows], acc[kRows];
+    const int row0 = band * (R * kWave) + lane * R;  // 0-based first DP row of this lane
+    unsigned rp[R][NP], gxk[R], h[R], acc[R];
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) {
+    for (int r = 0; r < R; ++r) {
       const int row = min(row0 + r, pd.m - 1);  // rows past m: copies of the last (never traced)
       const int4* pr = reinterpret_cast<const int4*>(a.prow + (pd.x_off + row) * 8);
       const int4 q0 = pr[0], q1 = pr[1];
@@ -2689,7 +2701,7 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
       h[r] = 4u * e[7];         // H[i][0]
       acc[r] = 0;
     }
-    unsigned Up = band == 0 ? 0u : 4u * (unsigned)a.prow[(pd.x_off + band * kBandRows - 1) * 8 + 7];  // H[row above the band][0]
+    unsigned Up = band == 0 ? 0u : 4u * (unsigned)a.prow[(pd.x_off + band * (R * kWave) - 1) * 8 + 7];  // H[row above the band][0]
     unsigned stH = 0;
     const bool from_above = band > 0;
     const bool to_below = band + 1 < pd.nbands;
@@ -2697,7 +2709,7 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
     const u64* gin = reinterpret_cast<const u64*>(a.bnd) + pd.bnd_off + (int64_t)(band > 0 ? band - 1 : 0) * bstride + lane;
     const int last_chunk = pd.nchunks > 0 ? pd.nchunks - 1 : 0;
     u64* gout = a.bnd + pd.bnd_off + (int64_t)band * bstride + lane;
-    unsigned* mptr = a.mat + pd.mat_off + (int64_t)band * band_dwords(W, pd.sblocks) + lane;
+    unsigned* mptr = a.mat + pd.mat_off + (int64_t)band * prof_band_dwords(pd.sblocks) + lane;
     // column j (1-based; 0 = the H[0][0] entry) is pcol entry y_off + j; window of sb: columns 64sb-63 .. 64sb+64
     const int4* colg = reinterpret_cast<const int4*>(a.pcol) + 2 * (pd.y_off - 63);
     // Granule prefetches are ordinary (compiler-tracked) loads here: this
@@ -2709,13 +2721,13 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
     // fill-vs-walk guard: cell (m, n) is lane t's row r of the last band at
     // step n - 1 + t; H = key / 4
     int cap_s = -1, cap_t = 0, cap_r = 0;
-    unsigned hs[kRows];
+    unsigned hs[R];
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) hs[r] = 0;
+    for (int r = 0; r < R; ++r) hs[r] = 0;
     if (a.endv && band == pd.nbands - 1) {
-      const int wr = (pd.m - 1) - band * kBandRows;
-      cap_t = wr / kRows;
-      cap_r = wr % kRows;
+      const int wr = (pd.m - 1) - band * (R * kWave);
+      cap_t = wr / R;
+      cap_r = wr % R;
       cap_s = pd.n - 1 + cap_t;
     }
 
@@ -2739,8 +2751,8 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
         const unsigned bv[8] = {bA.x, bA.y, bA.z, bA.w, bB.x, bB.y, bB.z, bB.w};
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          stH = __builtin_amdgcn_update_dpp(h[kRows - 1], stH, 0x130 /*wave_shl:1*/, 0xf, 0xf, false);
-          const unsigned uh = __builtin_amdgcn_update_dpp(bv[k], h[kRows - 1], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
+          stH = __builtin_amdgcn_update_dpp(h[R - 1], stH, 0x130 /*wave_shl:1*/, 0xf, 0xf, false);
+          const unsigned uh = __builtin_amdgcn_update_dpp(bv[k], h[R - 1], 0x138 /*wave_shr:1*/, 0xf, 0xf, false);
           const unsigned dg0 = Up;
           Up = uh;
           // this lane's column j = s - lane + 1 -> window entry j - (64sb - 63) = (s - 64sb) - lane + 64
@@ -2750,9 +2762,9 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
           // left move key increment: gy follows the packed counts (int 2 / 3), or int 6
           const unsigned lk = 4u * (unsigned)(DOT >= 4 ? c0.z : DOT == 2 ? c0.w : c1.z) + 2u;
           const bool valid = !MASK || (s0 + k) >= lane;
-          unsigned hp = uh, nh[kRows];
+          unsigned hp = uh, nh[R];
 #pragma unroll
-          for (int r = 0; r < kRows; ++r) {
+          for (int r = 0; r < R; ++r) {
             unsigned sub;
             if constexpr (DOT == 0) {
               const unsigned cy[kProfSyms] = {(unsigned)c0.x, (unsigned)c0.y, (unsigned)c0.z,
@@ -2776,18 +2788,18 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
             hp = nh[r];
           }
 #pragma unroll
-          for (int r = 0; r < kRows; ++r) h[r] = nh[r];  // (d above read the previous step's h[r - 1])
+          for (int r = 0; r < R; ++r) h[r] = nh[r];  // (d above read the previous step's h[r - 1])
           if (blk * 8 + k == capk) {  // (uniform) the step of cell (m, n): the fill-vs-walk guard's end value
 #pragma unroll
-            for (int r = 0; r < kRows; ++r) hs[r] = nh[r];
+            for (int r = 0; r < R; ++r) hs[r] = nh[r];
           }
           if (k == 7) {
 #pragma unroll
-            for (int r = 0; r < kRows; ++r) __builtin_nontemporal_store(acc[r] | 0xccccccccu, mptr + r * kWave);
+            for (int r = 0; r < R; ++r) __builtin_nontemporal_store(acc[r] | 0xccccccccu, mptr + r * kWave);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
-        mptr += (8 / SPD) * kRows * kWave;
+        mptr += (8 / SPD) * R * kWave;
       }
     };
 
@@ -2824,7 +2836,7 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
     if (cap_s >= 0) {
       unsigned v = hs[0];
 #pragma unroll
-      for (int r = 1; r < kRows; ++r) v = cap_r == r ? hs[r] : v;
+      for (int r = 1; r < R; ++r) v = cap_r == r ? hs[r] : v;
       if (lane == cap_t) __hip_atomic_fetch_add((gu32*)(a.endv + pd.slot), v >> 2, RLX_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2841,7 +2853,7 @@ __global__ __launch_bounds__(256) void nw_profile(FillArgs a) {
       // nwk_msa verbose >= 2: per merge 8 u64, {walk start, walk end} (s_memrealtime, 100 MHz), then
       // the walk's cycle counters (trace_pair_affine<true>)
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot] = __builtin_amdgcn_s_memrealtime();
-      trace_pair_affine<true>(a, pd, tbl[wid], lane, prog);
+      trace_pair_affine<true, R>(a, pd, tbl[wid], lane, prog);
       if (a.stamps && lane == 0) a.stamps[8 * pd.slot + 1] = __builtin_amdgcn_s_memrealtime();
       PROG(0x60000000u);
     }

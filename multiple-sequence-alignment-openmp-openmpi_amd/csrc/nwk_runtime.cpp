@@ -31,6 +31,7 @@
 
 #include "../../include/nwk.h"
 #include "nwk_internal.h"
+#include "nwk_prof.h"
 #include "sha512.h"
 
 using namespace nwk;
@@ -3134,7 +3135,7 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       d.y_off = yoff;
       d.m = LX;
       d.n = LY;
-      d.nbands = (int)ceil_div(LX, kBandRows);
+      d.nbands = (int)ceil_div(LX, kProfBandRows);
       d.nchunks = (int)ceil_div(LY, 64);
       d.sblocks = d.nchunks + 1;
       d.slot = q;
@@ -3145,12 +3146,12 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       d.mat_off = mat;
       d.bnd_off = bnd;
       d.ops_off = ops;
-      mat += (int64_t)d.nbands * band_dwords(4, d.sblocks);
+      mat += (int64_t)d.nbands * prof_band_dwords(d.sblocks);
       bnd += (int64_t)d.nbands * d.nchunks * 64;  // granules of each band's last row (the last band's unused)
       ops += round_up((int64_t)LX + LY, 16);
       ntasks += d.nbands;
       st.cells += (double)LX * LY;
-      st.matrix_bytes += 4 * (int64_t)d.nbands * band_dwords(4, d.sblocks);
+      st.matrix_bytes += 4 * (int64_t)d.nbands * prof_band_dwords(d.sblocks);
     }
     // ---- pack ints 0-5 of every profile entry for nw_profile<DOT> (rc_host / Prof::cnt keep the plain counts)
     // 5: every merge's columns are one sequence (a caterpillar guide tree's levels), so a

@@ -117,7 +117,7 @@ KERNEL_SOURCES = {
     "nw_align_pk": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
     "nw_align_affine": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
     "nw_align": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
-    "nw_profile": ("csrc/nwk_kernels.hip", "csrc/nwk_internal.h", "Makefile"),
+    "nw_profile": ("csrc/nwk_kernels.hip", "csrc/nwk_prof.h", "csrc/nwk_internal.h", "Makefile"),
 }
 
 
