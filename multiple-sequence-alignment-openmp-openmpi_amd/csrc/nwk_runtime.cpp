@@ -2977,11 +2977,6 @@ struct Prof {
   int len = 0, parent = -1;
 };
 
-inline int64_t sym_cost(int a, int b, int gap, int pxy, int pgap) {
-  if (a == gap || b == gap) return (a == gap && b == gap) ? 0 : pgap;
-  return a == b ? 0 : pxy;
-}
-
 // Column symbol counts of a profile (S symbols, the last = gap).
 // a leaf's column counts (merged profiles add their children's along the path)
 void leaf_counts(const uint8_t* seq, int len, const uint8_t* code_of, int S, std::vector<int>* cnt) {
@@ -3068,9 +3063,6 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
   HIP_TRY(hipSetDevice(c->device));
   int rc;
   const int max_round = k > 1 ? round_of[nc - 1] : 0;
-  int64_t cst[kProfSyms][kProfSyms];  // symbol pair costs (gap = S - 1)
-  for (int a2 = 0; a2 < S; ++a2)
-    for (int b = 0; b < S; ++b) cst[a2][b] = sym_cost(a2, b, gap, pxy, pgap);
   DevBuf &d_prow = c->d_msa[0], &d_pcol = c->d_msa[1], &d_mw = c->d_msa[2], &d_pd = c->d_pairs, &d_tk = c->d_tasks;
   double t_lvl = now_ms(), t_prep = 0, t_wait = 0, t_build = 0;  // (verbose >= 2: host phases per level)
   for (int rd = 1; rd <= max_round; ++rd) {
@@ -3094,12 +3086,16 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       std::vector<int>& rch = rc_host[q];
       rch.assign((size_t)LX * 8, 0);
       for (int i = 0; i < LX; ++i) {
+        // rc[b] = sum_a cnt[a] c(a, b) in closed form (the SoP symbol costs: 0 on the
+        // diagonal and gap vs gap, pxy between residues, pgap residue vs gap): with ng
+        // residues and cg gaps in the column, rc[b] = pxy (ng - cnt[b]) + pgap cg for a
+        // residue b, pgap ng for the gap
+        const int* xc = &cx[(size_t)i * S];
+        int64_t ng = 0;
+        for (int a2 = 0; a2 < gap; ++a2) ng += xc[a2];
         int64_t rcb[kProfSyms] = {0};
-        for (int a2 = 0; a2 < S; ++a2) {
-          const int64_t na = cx[(size_t)i * S + a2];
-          if (na)
-            for (int b = 0; b < S; ++b) rcb[b] += na * cst[a2][b];
-        }
+        for (int b = 0; b < gap; ++b) rcb[b] = (int64_t)pxy * (ng - xc[b]) + (int64_t)pgap * xc[gap];
+        rcb[gap] = (int64_t)pgap * ng;
         const int64_t gx = (int64_t)(nx - cx[(size_t)i * S + gap]) * ny * pgap;
         acc += gx;
         for (int b = 0; b < kProfSyms; ++b) rch[(size_t)i * 8 + b] = (int)(b < S ? rcb[b] : 0);

@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round-6 session n: nw_profile A/B runs (tree vs abv6/base variant): 4 rows per lane in nw_profile + its walk (tree) vs 8 (abv6/base, -DNWK_PROF_ROWS=8).
+# Round-6 session n: MSA A/B runs (tree vs abv6/base variant): closed-form profile row costs on the host.
 set -u
 cd "$(dirname "$0")/../../.."
 O=gpurun_out/r06n; mkdir -p $O
