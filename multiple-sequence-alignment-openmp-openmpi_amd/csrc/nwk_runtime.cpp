@@ -3183,10 +3183,15 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
         }
       }
     }
-    // ---- device buffers: [granules | matrices | ops]
+    // ---- device buffers: [granules | matrices | ops | results]; the results (task
+    // counter, err, and per merge done, endv = H(m, n), oplen, endij) follow the ops, so
+    // a level zeroes them with one memset and reads them back with the ops in one copy
     t_build = now_ms();
-    const int64_t bnd_b = round_up(bnd * 8 + 4096, 256), mat_b = round_up(mat * 4, 256);
-    const int64_t work_b = bnd_b + mat_b + ops + 4096;
+    const int64_t bnd_b = round_up(bnd * 8 + 4096, 256), mat_b = round_up(mat * 4, 256), ops_b = round_up(ops, 256);
+    const int64_t r_done = 256, r_endv = r_done + round_up(4 * (int64_t)np, 16), r_oplen = r_endv + round_up(4 * (int64_t)np, 16);
+    const int64_t r_endij = r_oplen + round_up(4 * (int64_t)np, 16), res_b = round_up(r_endij + 8 * (int64_t)np, 256);
+    const int64_t res_off = bnd_b + mat_b + ops_b;
+    const int64_t work_b = res_off + res_b + 4096;
     if ((rc = d_mw.ensure((size_t)work_b)) != NWK_OK) return rc;
     if ((rc = d_prow.ensure(4 * hrow.size() + 64)) != NWK_OK) return rc;
     if ((rc = d_pcol.ensure(4 * hcol.size() + 64)) != NWK_OK) return rc;
@@ -3196,16 +3201,13 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
     for (int q = 0; q < np; ++q)
       for (int b = 0; b < pd[q].nbands; ++b) tk.push_back(make_int2(q, b));
     for (auto& d : pd) { d.mat_off += bnd_b / 4; d.ops_off += bnd_b + mat_b; }
-    if ((rc = c->d_oplen.ensure(sizeof(int) * np)) != NWK_OK) return rc;
-    if ((rc = c->d_endij.ensure(sizeof(int2) * np)) != NWK_OK) return rc;
-    if ((rc = c->d_done.ensure(sizeof(unsigned) * np)) != NWK_OK) return rc;
+    uint8_t* const res_d = d_mw.as<uint8_t>() + res_off;
     HIP_TRY(hipMemsetAsync(d_mw.p, 0, (size_t)bnd_b, c->stream));  // granule tags start below any epoch
+    HIP_TRY(hipMemsetAsync(res_d, 0, (size_t)res_b, c->stream));
     HIP_TRY(hipMemcpyAsync(d_prow.p, hrow.data(), 4 * hrow.size(), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(d_pcol.p, hcol.data(), 4 * hcol.size(), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(d_pd.p, pd.data(), sizeof(PairDesc) * np, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(d_tk.p, tk.data(), sizeof(int2) * ntasks, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemsetAsync(c->d_ctl.p, 0, 256, c->stream));
-    HIP_TRY(hipMemsetAsync(c->d_done.p, 0, sizeof(unsigned) * np, c->stream));
     FillArgs fa{};
     memset(&fa, 0, sizeof fa);
     fa.pairs = d_pd.as<PairDesc>();
@@ -3213,12 +3215,12 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
     fa.ntasks = (int)ntasks;
     fa.mat = d_mw.as<uint32_t>();
     fa.bnd = d_mw.as<unsigned long long>();
-    fa.counter = c->d_ctl.as<unsigned>();
-    fa.err = c->d_ctl.as<unsigned>() + 16;
-    fa.done = c->d_done.as<unsigned>();
+    fa.counter = reinterpret_cast<unsigned*>(res_d);
+    fa.err = reinterpret_cast<unsigned*>(res_d) + 16;
+    fa.done = reinterpret_cast<unsigned*>(res_d + r_done);
     fa.ops = d_mw.as<uint8_t>();
-    fa.oplen = c->d_oplen.as<int>();
-    fa.endij = c->d_endij.as<int2>();
+    fa.oplen = reinterpret_cast<int*>(res_d + r_oplen);
+    fa.endij = reinterpret_cast<int2*>(res_d + r_endij);
     fa.epoch = 1;
     fa.ntasks_pairs = np;
     fa.prow = d_prow.as<int>();
@@ -3226,11 +3228,7 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
     fa.lin_mode = dot;  // the profile packing: nw_profile<5 | 4 | 2 | 0> (launch_fill)
     // fill-vs-walk guard: each merge's H(m, n) against the cost of its walked path (below)
     static const int msa_guard = getenv("NWK_GUARD") ? atoi(getenv("NWK_GUARD")) : 1;
-    if (msa_guard != 0) {
-      if ((rc = c->d_endv.ensure(sizeof(int) * np)) != NWK_OK) return rc;
-      HIP_TRY(hipMemsetAsync(c->d_endv.p, 0, sizeof(int) * np, c->stream));
-      fa.endv = c->d_endv.as<int>();
-    }
+    if (msa_guard != 0) fa.endv = reinterpret_cast<int*>(res_d + r_endv);
     const int grid = (int)std::min<int64_t>(fill_blocks_per_cu(kProfileDP, 4) * c->cus, ceil_div(ntasks, 4));
     if (getenv("NWK_WATCHDOG")) {
       if ((rc = c->d_prog.ensure(4 * (size_t)(grid + 1) * 4)) != NWK_OK) return rc;
@@ -3251,18 +3249,19 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
     HIP_TRY(launch_fill(kProfileDP, 4, fa, grid, c->stream));
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     watchdog_wait(c, fa.prog, grid);
-    std::vector<int> ol((size_t)np);
-    std::vector<int2> ej((size_t)np);
-    std::vector<uint8_t> hops((size_t)ops);
-    std::vector<int> mev((size_t)np, 0);
-    unsigned herr = 0;
-    HIP_TRY(hipMemcpyAsync(&herr, fa.err, 4, hipMemcpyDeviceToHost, c->stream));
-    if (fa.endv) HIP_TRY(hipMemcpyAsync(mev.data(), fa.endv, 4 * (size_t)np, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(ol.data(), fa.oplen, 4 * np, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(ej.data(), fa.endij, 8 * np, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(hops.data(), d_mw.as<uint8_t>() + bnd_b + mat_b, (size_t)ops, hipMemcpyDeviceToHost, c->stream));
+    // ops and results in one copy
+    std::vector<uint8_t> hops((size_t)(ops_b + res_b));
+    HIP_TRY(hipMemcpyAsync(hops.data(), d_mw.as<uint8_t>() + bnd_b + mat_b, hops.size(), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    const uint8_t* hres = hops.data() + ops_b;
+    unsigned herr = 0;
+    memcpy(&herr, hres + 64, 4);
     if (herr) return fail(NWK_EKERNEL, "nwk_msa: profile kernel fault (err=%u)", herr);
+    std::vector<int> ol((size_t)np), mev((size_t)np, 0);
+    std::vector<int2> ej((size_t)np);
+    memcpy(ol.data(), hres + r_oplen, 4 * (size_t)np);
+    memcpy(ej.data(), hres + r_endij, 8 * (size_t)np);
+    if (fa.endv) memcpy(mev.data(), hres + r_endv, 4 * (size_t)np);
     t_wait = now_ms();
     float lvl_ms = 0;
     HIP_TRY(hipEventElapsedTime(&lvl_ms, c->ev[0], c->ev[1]));
