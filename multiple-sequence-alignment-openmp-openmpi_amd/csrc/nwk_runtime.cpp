@@ -3064,7 +3064,7 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
   int rc;
   const int max_round = k > 1 ? round_of[nc - 1] : 0;
   DevBuf &d_prow = c->d_msa[0], &d_pcol = c->d_msa[1], &d_mw = c->d_msa[2], &d_pd = c->d_pairs, &d_tk = c->d_tasks;
-  double t_lvl = now_ms(), t_prep = 0, t_wait = 0, t_build = 0;  // (verbose >= 2: host phases per level)
+  double t_lvl = now_ms(), t_mg = t_lvl, t_prep = 0, t_wait = 0, t_build = 0;  // (verbose >= 2: host phases per level)
   for (int rd = 1; rd <= max_round; ++rd) {
     std::vector<Merge> ms;
     for (const auto& m : merges)
@@ -3283,10 +3283,10 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       const unsigned long long* x = &sw[8 * (size_t)qm];
       fprintf(stderr, "nwk_msa level %d: %d merges, %lld band tasks, %.3f ms (walks: longest %.3f ms, sum %.3f ms; "
               "longest: %llu cycles, tile switches %.1f%%, code reads %.1f%%, %llu blocks, %llu switches, %llu "
-              "moves); host: previous merges + profiles %.3f ms, uploads %.3f ms, launch to results "
-              "%.3f ms\n", rd, np, (long long)ntasks, (double)lvl_ms, wmax, wsum, x[2], x[2] ? 100.0 * x[3] / x[2] : 0.0,
+              "moves); host: previous merges + profiles %.3f ms (merges %.3f, profiles %.3f), uploads %.3f ms, launch "
+              "to results %.3f ms\n", rd, np, (long long)ntasks, (double)lvl_ms, wmax, wsum, x[2], x[2] ? 100.0 * x[3] / x[2] : 0.0,
               x[2] ? 100.0 * x[4] / x[2] : 0.0, x[5] >> 32, x[5] & 0xffffffffull, x[6] & 0xffffffffull,
-              t_build - t_lvl, t_prep - t_build, t_wait - t_prep);
+              t_build - t_lvl, t_mg - t_lvl, t_build - t_mg, t_prep - t_build, t_wait - t_prep);
     }
     // ---- merged profiles and merge costs (forward moves: prefix run, then the reversed trace)
     for (int q = 0; q < np; ++q) {
@@ -3353,6 +3353,7 @@ int nwk_msa(nwk_ctx* c, int32_t pxy, int32_t pgap, const int32_t* penalties, uin
       std::vector<int>().swap(Ym.cnt);
     }
     t_lvl = t_wait;
+    t_mg = now_ms();
   }
   st.total_ms = now_ms() - t_start;
   c->stats = st;
