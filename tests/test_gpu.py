@@ -754,6 +754,20 @@ def test_msa_many_sequences_vs_oracle(engine):
     assert (rows, s) == oracle.msa(genes, 3, 2)
 
 
+@pytest.mark.parametrize("L", [255, 256, 257, 511, 512, 513, 1023, 1025])
+def test_msa_band_edges_vs_oracle(engine, L):
+    """Profile lengths on either side of nw_profile's band edges (64 lanes x kProfRows = 4
+    rows: 256-row bands; 512 with 8 rows): the row above a band, the last band's H(m, n)
+    capture and the walk's band switches, bit-exact against the oracle."""
+    r = random.Random(7000 + L)
+    genes = [bytes(r.choice(ACGT) for _ in range(L))]
+    genes += [bytes(r.choice(ACGT) for _ in range(L + d)) for d in (0, -1)]
+    engine.set_sequences(genes)
+    rows, s = engine.msa(3, 2)
+    assert (rows, s) == oracle.msa(genes, 3, 2)
+    assert oracle.sop(rows, 3, 2) == s
+
+
 def test_msa_small_and_edge_sets(engine):
     for genes in ([b"ACGT"], [b"A", b"A"], [b"A", b"C"], [b"AC", b"A", b"C", b"CA"], [b"A" * 600, b"C"]):
         engine.set_sequences(genes)
