@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round-6 session n: MSA A/B runs (tree vs abv6/base variant): a level's results in one copy and one memset.
+# Round-6 session n: MSA A/B runs (tree vs abv6/base variant): block path as a scalar-mask orbit (NWK_WALK_JUMP 3) vs pointer doubling (2).
 set -u
 cd "$(dirname "$0")/../../.."
 O=gpurun_out/r06n; mkdir -p $O
