@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round-6 session n: MSA A/B runs (tree vs abv6/base variant): block path as a scalar-mask orbit (NWK_WALK_JUMP 3) vs pointer doubling (2).
+# Round-6 session n: MSA A/B runs (tree vs abv6/base variant): 2 rows per lane in nw_profile (tree) vs 4 (base).
 set -u
 cd "$(dirname "$0")/../../.."
 O=gpurun_out/r06n; mkdir -p $O
