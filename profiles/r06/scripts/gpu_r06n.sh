@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round-6 session n: MSA A/B runs (tree vs abv6/base variant): 2 rows per lane in nw_profile (tree) vs 4 (base).
+# Round-6 session n: MSA A/B runs: the tree vs abv6/base = the tree built with -DNWK_POLL_SLEEP_MAX=4 (shorter granule-poll sleeps).
 set -u
 cd "$(dirname "$0")/../../.."
 O=gpurun_out/r06n; mkdir -p $O
